@@ -1,0 +1,122 @@
+/*
+ * tneqhip.h — C ABI of libtneqhip.so, the MI355X (gfx950) contraction engine that sits
+ * under the tneq_qc backend / contractor plugin surface.
+ *
+ * Every entry point takes plain pointers and sizes (no torch types).  Device pointers are
+ * caller-owned (e.g. torch.Tensor.data_ptr()); plans and their arenas are library-owned.
+ * `stream` is a hipStream_t passed as void* (NULL = the default stream).
+ * Return value: 0 = ok, < 0 = error (tq_last_error() has the message).  The Python host maps
+ * TQ_ERR_INVALID to ValueError and everything else to RuntimeError, as the reference does
+ * (SURVEY.md §8(b) "Conventions": qctn.py:826-831 ValueError, compiler.py:120-121 RuntimeError).
+ *
+ * Which reference interface each entry point replaces (all paths under /root/reference):
+ *   tq_permute        — the strided transpose inside every pairwise step of
+ *                       opt_einsum's ContractExpression (called at
+ *                       tneq_qc/contractor/einsum_strategy.py:639-643 and
+ *                       symmetry_breaking_quantum.py:142,154,213) and the explicit
+ *                       permute(...).contiguous() at tneq_qc/distributed/engine/distributed_engine.py:1330,1635;
+ *                       BackendPyTorch.permute tneq_qc/backends/backend_pytorch.py:619-621.
+ *   tq_gemm_batched   — the GEMM / bmm under each tensordot (torch.tensordot -> at::mm) and the
+ *                       partial bmm at distributed_engine.py:1477-1487.
+ *   tq_contract_pair  — one pairwise tensordot with arbitrary output mode order
+ *                       (opt_einsum pairwise step; BackendPyTorch.einsum backend_pytorch.py:623-625
+ *                       for two operands; ComputeBackend.einsum backend_interface.py:495-507).
+ *   tq_plan_*         — a whole ContractExpression: ComputeBackend.execute_expression
+ *                       (backend_interface.py:102-114, backend_pytorch.py:99-105) over the
+ *                       expression created by EinsumStrategy.create_contract_expression
+ *                       (einsum_strategy.py:622-643), plus index slicing.
+ *   tq_axpy           — the partial-amplitude accumulation before the slice reduce
+ *                       (AllReduceGrad, tneq_qc/distributed/optim/allreduce_grad.py:13-60).
+ */
+#ifndef TNEQHIP_H
+#define TNEQHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types; complex types are interleaved (re, im) like numpy / torch complex64/128 */
+enum { TQ_F32 = 0, TQ_F64 = 1, TQ_C64 = 2, TQ_C128 = 3 };
+
+enum {
+  TQ_OK = 0,
+  TQ_ERR_INVALID = -1,     /* bad shape / mode / argument  -> ValueError */
+  TQ_ERR_HIP = -2,         /* HIP runtime error             -> RuntimeError */
+  TQ_ERR_ALLOC = -3,       /* device allocation failed      -> RuntimeError (MemoryError) */
+  TQ_ERR_UNSUPPORTED = -4  /* valid but not implemented     -> RuntimeError */
+};
+
+#define TQ_MAX_RANK 64
+
+/* ---- library ---------------------------------------------------------------------- */
+int tq_version(void);                      /* (major << 16) | minor */
+int tq_last_error(char* buf, size_t n);    /* copies the last error of this thread; returns its length */
+int tq_device_synchronize(void);
+
+/* ---- kernels ----------------------------------------------------------------------- */
+
+/* dst[c_0..c_{r-1}] = src[sum_d c_d * src_strides[d]] + beta * dst[...]
+ * dst is contiguous in the order of `shape` (row-major, last dim fastest).
+ * src_strides are in elements and may be 0 (broadcast) or describe any view (slice).  */
+int tq_permute(int dtype, int rank, const int64_t* shape, const int64_t* src_strides,
+               const void* src, void* dst, double beta, void* stream);
+
+/* C_b = A_b * B_b + beta * C_b for b in [0, batch);  row-major operands:
+ *   transA == 0: A_b is M x K with leading dim lda (K contiguous);  transA == 1: A_b is K x M (M contiguous)
+ *   transB == 0: B_b is K x N with leading dim ldb (N contiguous);  transB == 1: B_b is N x K (K contiguous)
+ *   C_b is M x N with leading dim ldc.
+ * No conjugation.  `workspace` may be NULL (then no split-K is used).               */
+int tq_gemm_batched(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K,
+                    int64_t batch, const void* A, int64_t lda, int64_t strideA, const void* B,
+                    int64_t ldb, int64_t strideB, double beta, void* C, int64_t ldc,
+                    int64_t strideC, void* workspace, size_t ws_bytes, void* stream);
+size_t tq_gemm_workspace_size(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
+
+/* y = x + beta * y over n elements (used to sum partial amplitudes of slices) */
+int tq_axpy(int dtype, int64_t n, const void* x, void* y, double beta, void* stream);
+
+/* One pairwise tensordot with arbitrary output order (einsum "A,B->C" with integer modes).
+ * A mode present in A and B but not C is summed; a mode present in A, B and C is a batch
+ * mode; a mode present in only one operand and not in C is summed over that operand.
+ * All tensors contiguous row-major.  Call tq_contract_pair_workspace() first.          */
+size_t tq_contract_pair_workspace(int dtype, int rankA, const int64_t* shapeA,
+                                  const int32_t* modesA, int rankB, const int64_t* shapeB,
+                                  const int32_t* modesB, int rankC, const int32_t* modesC);
+int tq_contract_pair(int dtype, int rankA, const int64_t* shapeA, const int32_t* modesA,
+                     const void* A, int rankB, const int64_t* shapeB, const int32_t* modesB,
+                     const void* B, int rankC, const int32_t* modesC, void* C,
+                     void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- plans: a GPU-resident contraction tree with preallocated intermediates --------- */
+typedef struct tq_plan_s* tq_plan;
+
+/* Inputs: n_inputs tensors; tensor i has in_ranks[i] modes taken consecutively from
+ * in_modes / in_extents / in_strides (strides in elements; pass NULL for contiguous).
+ * path: n_steps pairs of SSA ids (inputs are 0..n_inputs-1, step s creates id n_inputs+s),
+ * exactly opt_einsum's "ssa path".  The last step's result must hold exactly the out_modes.
+ * sliced_modes: contracted modes that are fixed per slice; slice ids enumerate them in
+ * row-major order of the given list.                                                    */
+int tq_plan_create(tq_plan* plan, int dtype, int n_inputs, const int32_t* in_ranks,
+                   const int32_t* in_modes, const int64_t* in_extents, const int64_t* in_strides,
+                   int out_rank, const int32_t* out_modes, int n_steps, const int32_t* path,
+                   int n_sliced, const int32_t* sliced_modes);
+
+/* Queries: key = "n_slices", "arena_bytes", "flops" (per slice, algorithmic), "bytes_moved",
+ * "n_kernels" (launches per slice), "n_gemm", "n_apply", "n_permute".  Returns -1 if unknown. */
+int64_t tq_plan_query(tq_plan plan, const char* key);
+/* human-readable per-step description into buf (for debugging / DESIGN evidence) */
+int tq_plan_describe(tq_plan plan, char* buf, size_t n);
+
+/* Runs slices slice_begin, slice_begin + slice_step, ... < slice_end and sums them into out
+ * (out = sum + (accumulate ? out : 0)).  inputs[i] are device pointers of the FULL inputs.  */
+int tq_plan_execute(tq_plan plan, const void* const* inputs, void* out, int64_t slice_begin,
+                    int64_t slice_end, int64_t slice_step, int accumulate, void* stream);
+int tq_plan_destroy(tq_plan plan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TNEQHIP_H */

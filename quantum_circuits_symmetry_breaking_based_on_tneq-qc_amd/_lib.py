@@ -1,0 +1,112 @@
+"""ctypes binding of libtneqhip.so (C ABI in include/tneqhip.h).
+
+The product path has no CPU fallback: if the library is missing or cannot be loaded the
+import of :func:`lib` raises, and every backend / strategy entry point calls it.
+torch is imported first so that libtneqhip.so binds to the HIP runtime torch already loaded
+(same SONAME libamdhip64.so.7), giving one runtime per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TNEQHIP_LIB", os.path.join(_HERE, "lib", "libtneqhip.so"))
+
+TQ_F32, TQ_F64, TQ_C64, TQ_C128 = 0, 1, 2, 3
+TQ_OK, TQ_ERR_INVALID, TQ_ERR_HIP, TQ_ERR_ALLOC, TQ_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
+
+# every symbol the header declares (tests check the .so exports all of them)
+EXPORTED = (
+    "tq_version", "tq_last_error", "tq_device_synchronize", "tq_permute", "tq_gemm_batched",
+    "tq_gemm_workspace_size", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
+    "tq_plan_create", "tq_plan_query", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
+)
+
+
+class TneqHipError(RuntimeError):
+    """A HIP / library failure (maps TQ_ERR_HIP / TQ_ERR_UNSUPPORTED / TQ_ERR_ALLOC)."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+_c = ctypes
+_i64p = _c.POINTER(_c.c_int64)
+_i32p = _c.POINTER(_c.c_int32)
+_vp = _c.c_void_p
+
+_SIGS = {
+    "tq_version": (_c.c_int, []),
+    "tq_last_error": (_c.c_int, [_c.c_char_p, _c.c_size_t]),
+    "tq_device_synchronize": (_c.c_int, []),
+    "tq_permute": (_c.c_int, [_c.c_int, _c.c_int, _i64p, _i64p, _vp, _vp, _c.c_double, _vp]),
+    "tq_gemm_batched": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64,
+                                   _c.c_int64, _vp, _c.c_int64, _c.c_int64, _vp, _c.c_int64,
+                                   _c.c_int64, _c.c_double, _vp, _c.c_int64, _c.c_int64, _vp,
+                                   _c.c_size_t, _vp]),
+    "tq_gemm_workspace_size": (_c.c_size_t, [_c.c_int, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64]),
+    "tq_axpy": (_c.c_int, [_c.c_int, _c.c_int64, _vp, _vp, _c.c_double, _vp]),
+    "tq_contract_pair_workspace": (_c.c_size_t, [_c.c_int, _c.c_int, _i64p, _i32p, _c.c_int, _i64p,
+                                                 _i32p, _c.c_int, _i32p]),
+    "tq_contract_pair": (_c.c_int, [_c.c_int, _c.c_int, _i64p, _i32p, _vp, _c.c_int, _i64p, _i32p,
+                                    _vp, _c.c_int, _i32p, _vp, _vp, _c.c_size_t, _vp]),
+    "tq_plan_create": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _i32p, _i32p, _i64p, _i64p,
+                                  _c.c_int, _i32p, _c.c_int, _i32p, _c.c_int, _i32p]),
+    "tq_plan_query": (_c.c_int64, [_vp, _c.c_char_p]),
+    "tq_plan_describe": (_c.c_int, [_vp, _c.c_char_p, _c.c_size_t]),
+    "tq_plan_execute": (_c.c_int, [_vp, _c.POINTER(_vp), _vp, _c.c_int64, _c.c_int64, _c.c_int64,
+                                   _c.c_int, _vp]),
+    "tq_plan_destroy": (_c.c_int, [_vp]),
+}
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the native library is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (bind to torch's HIP runtime)
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libtneqhip.so not found at {LIB_PATH}: build it with "
+                f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = h
+    return _lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(4096)
+    lib().tq_last_error(buf, 4096)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    """Map a C status to the reference's exception types (ValueError / RuntimeError)."""
+    if rc == TQ_OK:
+        return
+    msg = f"{what}: {last_error()}" if what else last_error()
+    if rc == TQ_ERR_INVALID:
+        raise ValueError(msg)
+    if rc == TQ_ERR_ALLOC:
+        raise MemoryError(msg)
+    raise TneqHipError(msg)
+
+
+def i64(seq):
+    seq = [int(x) for x in seq]
+    return (ctypes.c_int64 * max(1, len(seq)))(*seq)
+
+
+def i32(seq):
+    seq = [int(x) for x in seq]
+    return (ctypes.c_int32 * max(1, len(seq)))(*seq)

@@ -1,0 +1,198 @@
+// extern "C" surface of libtneqhip.so (declared in include/tneqhip.h).
+#include <cstring>
+#include <exception>
+#include <new>
+
+#include "tq_common.h"
+#include "tq_plan.h"
+
+namespace tq {
+namespace {
+thread_local std::string g_last_error;
+}
+void set_error(const std::string& msg) { g_last_error = msg; }
+const std::string& last_error() { return g_last_error; }
+}  // namespace tq
+
+struct tq_plan_s {
+  tq::Plan plan;
+  bool materialized = false;
+};
+
+#define TQ_GUARD_BEGIN try {
+#define TQ_GUARD_END                                                   \
+  }                                                                    \
+  catch (const std::bad_alloc&) {                                      \
+    tq::set_error("host allocation failed");                           \
+    return TQ_ERR_ALLOC;                                               \
+  }                                                                    \
+  catch (const std::exception& e) {                                    \
+    tq::set_error(std::string("exception: ") + e.what());              \
+    return TQ_ERR_INVALID;                                             \
+  }
+
+extern "C" {
+
+int tq_version(void) { return (0 << 16) | 1; }
+
+int tq_last_error(char* buf, size_t n) {
+  const std::string& e = tq::last_error();
+  if (buf && n) {
+    const size_t k = std::min(n - 1, e.size());
+    std::memcpy(buf, e.data(), k);
+    buf[k] = 0;
+  }
+  return (int)e.size();
+}
+
+int tq_device_synchronize(void) {
+  TQ_HIP(hipDeviceSynchronize());
+  return TQ_OK;
+}
+
+int tq_permute(int dtype, int rank, const int64_t* shape, const int64_t* src_strides,
+               const void* src, void* dst, double beta, void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(rank == 0 || (shape && src_strides), "null shape/strides");
+  return tq::permute_launch(dtype, rank, shape, src_strides, src, dst, beta, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+int tq_gemm_batched(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K,
+                    int64_t batch, const void* A, int64_t lda, int64_t strideA, const void* B,
+                    int64_t ldb, int64_t strideB, double beta, void* C, int64_t ldc,
+                    int64_t strideC, void* workspace, size_t ws_bytes, void* stream) {
+  TQ_GUARD_BEGIN
+  return tq::gemm_launch(dtype, transA, transB, M, N, K, batch, A, lda, strideA, B, ldb, strideB,
+                         beta, C, ldc, strideC, workspace, ws_bytes, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+size_t tq_gemm_workspace_size(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (!tq::dtype_valid(dtype)) return 0;
+  return tq::gemm_workspace(dtype, M, N, K, batch);
+}
+
+int tq_axpy(int dtype, int64_t n, const void* x, void* y, double beta, void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(tq::dtype_valid(dtype), "dtype");
+  return tq::axpy_launch(dtype, n, x, y, beta, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+static int pair_plan(tq::Plan& P, int dtype, int rankA, const int64_t* shapeA, const int32_t* modesA,
+                     int rankB, const int64_t* shapeB, const int32_t* modesB, int rankC,
+                     const int32_t* modesC) {
+  TQ_CHECK_ARG(rankA >= 0 && rankB >= 0 && rankC >= 0, "rank");
+  std::vector<int32_t> ranks = {rankA, rankB};
+  std::vector<int32_t> modes(modesA, modesA + rankA);
+  modes.insert(modes.end(), modesB, modesB + rankB);
+  std::vector<int64_t> ext(shapeA, shapeA + rankA);
+  ext.insert(ext.end(), shapeB, shapeB + rankB);
+  const int32_t path[2] = {0, 1};
+  return tq::plan_compile(P, dtype, 2, ranks.data(), modes.data(), ext.data(), nullptr, rankC,
+                          modesC, 1, path, 0, nullptr);
+}
+
+size_t tq_contract_pair_workspace(int dtype, int rankA, const int64_t* shapeA,
+                                  const int32_t* modesA, int rankB, const int64_t* shapeB,
+                                  const int32_t* modesB, int rankC, const int32_t* modesC) {
+  try {
+    tq::Plan P;
+    if (pair_plan(P, dtype, rankA, shapeA, modesA, rankB, shapeB, modesB, rankC, modesC) != TQ_OK)
+      return 0;
+    return P.arena_bytes + P.table_bytes + 256;
+  } catch (...) {
+    return 0;
+  }
+}
+
+int tq_contract_pair(int dtype, int rankA, const int64_t* shapeA, const int32_t* modesA,
+                     const void* A, int rankB, const int64_t* shapeB, const int32_t* modesB,
+                     const void* B, int rankC, const int32_t* modesC, void* C, void* workspace,
+                     size_t ws_bytes, void* stream) {
+  TQ_GUARD_BEGIN
+  tq::Plan P;
+  TQ_TRY(pair_plan(P, dtype, rankA, shapeA, modesA, rankB, shapeB, modesB, rankC, modesC));
+  const size_t need = P.arena_bytes + P.table_bytes + 256;
+  TQ_CHECK_ARG(ws_bytes >= need || (P.arena_bytes + P.table_bytes) == 0, "workspace too small");
+  char* ws = (char*)workspace;
+  char* arena = ws;
+  char* tables = ws + (P.arena_bytes + 255) / 256 * 256;
+  TQ_TRY(tq::plan_materialize(P, P.arena_bytes ? arena : nullptr,
+                              P.table_bytes ? tables : nullptr, (hipStream_t)stream));
+  if (!P.arena_bytes && !P.table_bytes) P.owns_device = false;
+  const void* ins[2] = {A, B};
+  return tq::plan_run(P, ins, C, 0, 1, 1, 0, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+int tq_plan_create(tq_plan* out, int dtype, int n_inputs, const int32_t* in_ranks,
+                   const int32_t* in_modes, const int64_t* in_extents, const int64_t* in_strides,
+                   int out_rank, const int32_t* out_modes, int n_steps, const int32_t* path,
+                   int n_sliced, const int32_t* sliced_modes) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(out != nullptr, "null plan pointer");
+  *out = nullptr;
+  auto* h = new tq_plan_s();
+  int rc = tq::plan_compile(h->plan, dtype, n_inputs, in_ranks, in_modes, in_extents, in_strides,
+                            out_rank, out_modes, n_steps, path, n_sliced, sliced_modes);
+  if (rc != TQ_OK) {
+    tq::plan_release(h->plan);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return TQ_OK;
+  TQ_GUARD_END
+}
+
+int64_t tq_plan_query(tq_plan p, const char* key) {
+  if (!p || !key) return -1;
+  const tq::Plan& P = p->plan;
+  const std::string k(key);
+  if (k == "n_slices") return P.n_slices;
+  if (k == "arena_bytes") return (int64_t)P.arena_bytes;
+  if (k == "table_bytes") return (int64_t)P.table_bytes;
+  if (k == "flops") return (int64_t)P.flops;
+  if (k == "bytes_moved") return (int64_t)P.bytes;
+  if (k == "n_kernels") return (int64_t)P.ops.size();
+  if (k == "n_gemm") return P.n_gemm;
+  if (k == "n_apply") return P.n_apply;
+  if (k == "n_permute") return P.n_permute;
+  if (k == "out_numel") return P.out_numel;
+  return -1;
+}
+
+int tq_plan_describe(tq_plan p, char* buf, size_t n) {
+  if (!p) return TQ_ERR_INVALID;
+  const std::string& d = p->plan.describe;
+  if (buf && n) {
+    const size_t k = std::min(n - 1, d.size());
+    std::memcpy(buf, d.data(), k);
+    buf[k] = 0;
+  }
+  return (int)d.size();
+}
+
+int tq_plan_execute(tq_plan p, const void* const* inputs, void* out, int64_t slice_begin,
+                    int64_t slice_end, int64_t slice_step, int accumulate, void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(p != nullptr, "null plan");
+  if (!p->materialized) {  // device memory is taken at first use, so plans compile without a GPU
+    TQ_TRY(tq::plan_materialize(p->plan, nullptr, nullptr, (hipStream_t)stream));
+    p->materialized = true;
+  }
+  return tq::plan_run(p->plan, inputs, out, slice_begin, slice_end, slice_step, accumulate,
+                      (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+int tq_plan_destroy(tq_plan p) {
+  if (!p) return TQ_OK;
+  tq::plan_release(p->plan);
+  delete p;
+  return TQ_OK;
+}
+
+}  // extern "C"

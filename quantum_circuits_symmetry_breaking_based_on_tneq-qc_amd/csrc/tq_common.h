@@ -1,0 +1,105 @@
+// Shared internals of libtneqhip: error state, element traits, small helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/tneqhip.h"
+
+namespace tq {
+
+// ---- error reporting (thread-local last error, surfaced through tq_last_error) ----------
+void set_error(const std::string& msg);
+const std::string& last_error();
+
+#define TQ_CHECK_ARG(cond, msg)                                   \
+  do {                                                            \
+    if (!(cond)) {                                                \
+      ::tq::set_error(std::string("invalid argument: ") + (msg)); \
+      return TQ_ERR_INVALID;                                      \
+    }                                                             \
+  } while (0)
+
+#define TQ_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      ::tq::set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " +     \
+                      __FILE__ + ":" + std::to_string(__LINE__));                      \
+      return TQ_ERR_HIP;                                                               \
+    }                                                                                  \
+  } while (0)
+
+#define TQ_TRY(expr)        \
+  do {                      \
+    int rc_ = (expr);       \
+    if (rc_ != TQ_OK) return rc_; \
+  } while (0)
+
+inline size_t dtype_size(int dt) {
+  switch (dt) {
+    case TQ_F32: return 4;
+    case TQ_F64: return 8;
+    case TQ_C64: return 8;
+    case TQ_C128: return 16;
+    default: return 0;
+  }
+}
+inline bool dtype_complex(int dt) { return dt == TQ_C64 || dt == TQ_C128; }
+inline bool dtype_valid(int dt) { return dt >= TQ_F32 && dt <= TQ_C128; }
+
+// Storage element types for the kernels.  Complex values are interleaved (re, im).
+struct c64 { float re, im; };
+struct c128 { double re, im; };
+
+template <typename T> struct Traits;
+template <> struct Traits<float>  { using R = float;  static constexpr bool cplx = false; static constexpr int code = TQ_F32; };
+template <> struct Traits<double> { using R = double; static constexpr bool cplx = false; static constexpr int code = TQ_F64; };
+template <> struct Traits<c64>    { using R = float;  static constexpr bool cplx = true;  static constexpr int code = TQ_C64; };
+template <> struct Traits<c128>   { using R = double; static constexpr bool cplx = true;  static constexpr int code = TQ_C128; };
+
+__host__ __device__ inline c64 operator+(c64 a, c64 b) { return {a.re + b.re, a.im + b.im}; }
+__host__ __device__ inline c128 operator+(c128 a, c128 b) { return {a.re + b.re, a.im + b.im}; }
+__host__ __device__ inline c64 operator*(c64 a, float s) { return {a.re * s, a.im * s}; }
+__host__ __device__ inline c128 operator*(c128 a, double s) { return {a.re * s, a.im * s}; }
+
+// complex fused multiply-add acc += a*b (no conjugation)
+__device__ __forceinline__ void cmac(float& acc, float a, float b) { acc = fmaf(a, b, acc); }
+__device__ __forceinline__ void cmac(double& acc, double a, double b) { acc = fma(a, b, acc); }
+__device__ __forceinline__ void cmac(c64& acc, c64 a, c64 b) {
+  acc.re = fmaf(a.re, b.re, acc.re); acc.re = fmaf(-a.im, b.im, acc.re);
+  acc.im = fmaf(a.re, b.im, acc.im); acc.im = fmaf(a.im, b.re, acc.im);
+}
+__device__ __forceinline__ void cmac(c128& acc, c128 a, c128 b) {
+  acc.re = fma(a.re, b.re, acc.re); acc.re = fma(-a.im, b.im, acc.re);
+  acc.im = fma(a.re, b.im, acc.im); acc.im = fma(a.im, b.re, acc.im);
+}
+template <typename T> __host__ __device__ inline T tzero() { return T{}; }
+
+inline int64_t prod(const std::vector<int64_t>& v) {
+  int64_t p = 1;
+  for (auto x : v) p *= x;
+  return p;
+}
+
+// ---- kernel launchers implemented in the .hip files -------------------------------------
+// permute (tq_permute.hip)
+int permute_launch(int dtype, int rank, const int64_t* shape, const int64_t* src_strides,
+                   const void* src, void* dst, double beta, hipStream_t stream);
+// gemm (tq_gemm.hip)
+int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
+                const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
+                int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
+                void* workspace, size_t ws_bytes, hipStream_t stream);
+size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
+// apply a small operand along a contiguous mode group (tq_apply.hip):
+//   C[o][n][i] = sum_k S[o][k][i] * G[k][n]     (S, C contiguous; G contiguous K x N)
+int apply_launch(int dtype, int64_t O, int64_t K, int64_t N, int64_t I, const void* S,
+                 const void* G, void* C, double beta, hipStream_t stream);
+int axpy_launch(int dtype, int64_t n, const void* x, void* y, double beta, hipStream_t stream);
+
+}  // namespace tq

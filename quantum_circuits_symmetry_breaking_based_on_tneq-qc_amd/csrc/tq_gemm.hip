@@ -1,0 +1,407 @@
+// Batched GEMM on gfx950 matrix cores for the inner product of every pairwise contraction.
+//
+// Replaces the GEMM under each tensordot of the reference's opt_einsum pairwise loop
+// (tneq_qc/contractor/einsum_strategy.py:639-643 -> torch.tensordot -> at::mm) and the
+// explicit partial bmm of the K-sharded reduce (tneq_qc/distributed/engine/distributed_engine.py:1477-1487).
+//
+//  * f32 / complex64  : v_mfma_f32_32x32x2_f32 (exact f32, 64 FLOP/clk/SIMD = FP32 peak).
+//                       block 128x128, 4 waves of 64x64, BK = 16.
+//  * f64 / complex128 : v_mfma_f64_16x16x4_f64. block 64x64, 4 waves of 32x32, BK = 16.
+//  * complex = 4 real MFMAs per complex k-step on split re/im LDS planes
+//      Cr += Ar*Br + (-Ai)*Bi ; Ci += Ar*Bi + Ai*Br     (8 real flops per complex MAC).
+//  * operands staged global -> registers -> LDS (next tile's global loads are issued before the
+//    current tile's MFMAs, written after the barrier), 16-byte vector loads where aligned.
+//  * split-K over blockIdx.z with fp partial slabs + a deterministic reduce kernel when the
+//    output tile count alone cannot fill 256 CUs.
+//  * XCD-aware tile order: tiles that share an A row panel are dealt to the same XCD.
+#include <algorithm>
+
+#include "tq_common.h"
+
+namespace tq {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <typename R> struct Cfg;
+template <> struct Cfg<float> {
+  static constexpr int MT = 32, KT = 2;          // MFMA tile M=N and K
+  static constexpr int TI = 2, TJ = 2;           // MFMA tiles per wave (rows, cols)
+  static constexpr int WM = MT * TI, WN = MT * TJ;
+  static constexpr int BM = 2 * WM, BN = 2 * WN; // 2x2 waves
+  static constexpr int BK = 16;
+  static constexpr int PAD = 0;                  // ds_read_b32 halves read distinct rows: no conflict
+  static constexpr int NACC = 16;                // accumulator values per MFMA tile per lane
+};
+template <> struct Cfg<double> {
+  static constexpr int MT = 16, KT = 4;
+  static constexpr int TI = 2, TJ = 2;
+  static constexpr int WM = MT * TI, WN = MT * TJ;
+  static constexpr int BM = 2 * WM, BN = 2 * WN;
+  static constexpr int BK = 16;
+  static constexpr int PAD = 16;                 // rows k, k+1 of a ds_read_b64 half -> other banks
+  static constexpr int NACC = 4;
+};
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  void* W;  // split-K partial slabs (splits x batch x M x N elements) or null
+  int64_t M, N, K, lda, ldb, ldc, sA, sB, sC, batch;
+  int64_t kchunk;
+  int splits;
+  int mt, nt;  // tile counts
+  int vecA, vecB;
+  double beta;
+};
+
+constexpr int kThreads = 256;
+
+template <typename R>
+__device__ __forceinline__ void mfma(R a, R b, typename std::conditional<sizeof(R) == 4, f32x16, f64x4>::type& c);
+template <>
+__device__ __forceinline__ void mfma<float>(float a, float b, f32x16& c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ void mfma<double>(double a, double b, f64x4& c) {
+  c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <typename R, bool CPLX, bool TA, bool TB>
+__global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
+  using C_ = Cfg<R>;
+  using AccT = typename std::conditional<sizeof(R) == 4, f32x16, f64x4>::type;
+  constexpr int EW = CPLX ? 2 : 1;                 // R values per element
+  constexpr int VE = 16 / (EW * (int)sizeof(R));   // elements per 16-byte vector
+  constexpr int BM = C_::BM, BN = C_::BN, BK = C_::BK;
+  constexpr int LM = BM + C_::PAD, LN = BN + C_::PAD;  // LDS row strides
+  constexpr int NVA = BM * BK / (VE * kThreads);
+  constexpr int NVB = BK * BN / (VE * kThreads);
+  constexpr int NPL = CPLX ? 2 : 1;
+
+  __shared__ __attribute__((aligned(16))) R sA[NPL][BK][LM];
+  __shared__ __attribute__((aligned(16))) R sB[NPL][BK][LN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  // ---- tile coordinates (XCD-aware: consecutive tiles along N of one M panel share an XCD)
+  const int ntiles = g.mt * g.nt;
+  int bid = blockIdx.x;
+  {
+    // bijective remap so that blocks b, b+8, b+16... (one XCD) get consecutive tiles
+    const int q = ntiles / 8, r = ntiles % 8;
+    const int xcd = bid % 8, idx = bid / 8;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    if (ntiles >= 8) bid = base + idx;
+  }
+  const int tm = bid / g.nt, tn = bid % g.nt;
+  const int zb = blockIdx.z;
+  const int split = zb % g.splits;
+  const int64_t b = zb / g.splits;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = split * g.kchunk;
+  const int64_t kend = min(g.K, kbeg + g.kchunk);
+
+  const R* A = reinterpret_cast<const R*>(g.A) + b * g.sA * EW;
+  const R* B = reinterpret_cast<const R*>(g.B) + b * g.sB * EW;
+
+  AccT acc_re[C_::TI][C_::TJ];
+  AccT acc_im[C_::TI][C_::TJ];
+#pragma unroll
+  for (int i = 0; i < C_::TI; ++i)
+#pragma unroll
+    for (int j = 0; j < C_::TJ; ++j) {
+#pragma unroll
+      for (int r = 0; r < C_::NACC; ++r) { acc_re[i][j][r] = 0; acc_im[i][j][r] = 0; }
+    }
+
+  R ra[NVA][VE * EW];
+  R rb[NVB][VE * EW];
+
+  // element (row, col) of a row-major matrix with leading dim ld, guarded
+  auto load_vec = [&](const R* X, int64_t ld, int64_t row, int64_t col, int64_t rows,
+                      int64_t cols, bool vec_ok, R* out) {
+    // VE elements along `col`
+    if (vec_ok && row < rows && col + VE <= cols) {
+      const float4 v = *reinterpret_cast<const float4*>(X + (row * ld + col) * EW);
+      const R* pv = reinterpret_cast<const R*>(&v);
+#pragma unroll
+      for (int e = 0; e < VE * EW; ++e) out[e] = pv[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        const bool in = row < rows && col + e < cols;
+#pragma unroll
+        for (int c = 0; c < EW; ++c) out[e * EW + c] = in ? X[(row * ld + col + e) * EW + c] : R(0);
+      }
+    }
+  };
+
+  auto global_load = [&](int64_t k0) {
+#pragma unroll
+    for (int s = 0; s < NVA; ++s) {
+      const int q = tid + s * kThreads;
+      if constexpr (!TA) {  // A is M x K, K contiguous: vectors along k
+        const int m = q % BM, kv = q / BM;
+        load_vec(A, g.lda, m0 + m, k0 + kv * VE, g.M, kend, g.vecA, ra[s]);
+      } else {              // A is K x M, M contiguous: vectors along m
+        const int mv = q % (BM / VE), k = q / (BM / VE);
+        load_vec(A, g.lda, k0 + k, m0 + mv * VE, kend, g.M, g.vecA, ra[s]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NVB; ++s) {
+      const int q = tid + s * kThreads;
+      if constexpr (!TB) {  // B is K x N, N contiguous
+        const int nv = q % (BN / VE), k = q / (BN / VE);
+        load_vec(B, g.ldb, k0 + k, n0 + nv * VE, kend, g.N, g.vecB, rb[s]);
+      } else {              // B is N x K, K contiguous
+        const int n = q % BN, kv = q / BN;
+        load_vec(B, g.ldb, n0 + n, k0 + kv * VE, g.N, kend, g.vecB, rb[s]);
+      }
+    }
+  };
+
+  auto lds_store = [&]() {
+#pragma unroll
+    for (int s = 0; s < NVA; ++s) {
+      const int q = tid + s * kThreads;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        int m, k;
+        if constexpr (!TA) { m = q % BM; k = (q / BM) * VE + e; }
+        else { m = (q % (BM / VE)) * VE + e; k = q / (BM / VE); }
+        sA[0][k][m] = ra[s][e * EW];
+        if constexpr (CPLX) sA[1][k][m] = ra[s][e * EW + 1];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NVB; ++s) {
+      const int q = tid + s * kThreads;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        int n, k;
+        if constexpr (!TB) { n = (q % (BN / VE)) * VE + e; k = q / (BN / VE); }
+        else { n = q % BN; k = (q / BN) * VE + e; }
+        sB[0][k][n] = rb[s][e * EW];
+        if constexpr (CPLX) sB[1][k][n] = rb[s][e * EW + 1];
+      }
+    }
+  };
+
+  // fragment lane maps (cdna_hip_programming.md §3):
+  //   f32 32x32x2 : A[i = l&31][k = l>>5], B[k = l>>5][j = l&31]
+  //   f64 16x16x4 : A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]
+  const int fr = lane % C_::MT;
+  const int fk = lane / C_::MT;
+
+  auto compute_tile = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += C_::KT) {
+      R ar[C_::TI], ai[C_::TI], br[C_::TJ], bi[C_::TJ];
+#pragma unroll
+      for (int i = 0; i < C_::TI; ++i) {
+        const int m = wr * C_::WM + i * C_::MT + fr;
+        ar[i] = sA[0][kk + fk][m];
+        if constexpr (CPLX) ai[i] = sA[1][kk + fk][m];
+      }
+#pragma unroll
+      for (int j = 0; j < C_::TJ; ++j) {
+        const int n = wc * C_::WN + j * C_::MT + fr;
+        br[j] = sB[0][kk + fk][n];
+        if constexpr (CPLX) bi[j] = sB[1][kk + fk][n];
+      }
+#pragma unroll
+      for (int i = 0; i < C_::TI; ++i)
+#pragma unroll
+        for (int j = 0; j < C_::TJ; ++j) {
+          mfma<R>(ar[i], br[j], acc_re[i][j]);
+          if constexpr (CPLX) {
+            mfma<R>(-ai[i], bi[j], acc_re[i][j]);
+            mfma<R>(ar[i], bi[j], acc_im[i][j]);
+            mfma<R>(ai[i], br[j], acc_im[i][j]);
+          }
+        }
+    }
+  };
+
+  if (kbeg < kend) {
+    global_load(kbeg);
+    for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+      lds_store();
+      __syncthreads();
+      if (k0 + BK < kend) global_load(k0 + BK);  // in flight during the MFMAs below
+      compute_tile();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue
+  R* Cout;
+  int64_t ldo;
+  const bool partial = g.splits > 1;
+  if (partial) {
+    Cout = reinterpret_cast<R*>(g.W) + ((int64_t)split * g.batch + b) * g.M * g.N * EW;
+    ldo = g.N;
+  } else {
+    Cout = reinterpret_cast<R*>(g.C) + b * g.sC * EW;
+    ldo = g.ldc;
+  }
+  const R beta = partial ? R(0) : (R)g.beta;
+#pragma unroll
+  for (int i = 0; i < C_::TI; ++i)
+#pragma unroll
+    for (int j = 0; j < C_::TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < C_::NACC; ++r) {
+        int row, col;
+        if constexpr (sizeof(R) == 4) {
+          row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          col = lane & 31;
+        } else {
+          row = (lane >> 4) + 4 * r;
+          col = lane & 15;
+        }
+        const int64_t gm = m0 + wr * C_::WM + i * C_::MT + row;
+        const int64_t gn = n0 + wc * C_::WN + j * C_::MT + col;
+        if (gm < g.M && gn < g.N) {
+          R* p = Cout + (gm * ldo + gn) * EW;
+          R vr = acc_re[i][j][r];
+          if constexpr (CPLX) {
+            R vi = acc_im[i][j][r];
+            if (beta != R(0)) { vr += beta * p[0]; vi += beta * p[1]; }
+            p[0] = vr;
+            p[1] = vi;
+          } else {
+            if (beta != R(0)) vr += beta * p[0];
+            p[0] = vr;
+          }
+        }
+      }
+}
+
+// C_b = sum_s W[s][b] + beta * C_b
+template <typename R>
+__global__ void __launch_bounds__(kThreads)
+splitk_reduce_kernel(const R* __restrict__ W, R* __restrict__ C, int64_t M, int64_t N,
+                     int64_t ldc, int64_t sC, int64_t batch, int splits, int ew, R beta) {
+  const int64_t per = M * N * ew;
+  const int64_t total = per * batch;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kThreads) {
+    const int64_t b = i / per, r = i % per;
+    const int64_t e = r / ew, c = r % ew;
+    const int64_t m = e / N, n = e % N;
+    R s = 0;
+    for (int k = 0; k < splits; ++k) s += W[(int64_t)k * total + i];
+    R* p = C + b * sC * ew + (m * ldc + n) * ew + c;
+    *p = beta != R(0) ? s + beta * *p : s;
+  }
+}
+
+template <typename R> int ew_of(int dtype) { return dtype_complex(dtype) ? 2 : 1; }
+
+int choose_splits(int64_t tiles, int64_t K, int BK) {
+  // aim for >= 512 workgroups (2 per CU) but keep >= 8 K-tiles per split
+  int s = 1;
+  while (tiles * s < 512 && K / ((int64_t)(s * 2) * BK) >= 8 && s < 64) s *= 2;
+  return s;
+}
+
+template <typename R, bool CPLX>
+int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
+                 const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB,
+                 double beta, void* C, int64_t ldc, int64_t sC, void* W, size_t wsb,
+                 hipStream_t stream) {
+  using C_ = Cfg<R>;
+  constexpr int EW = CPLX ? 2 : 1;
+  constexpr int VE = 16 / (EW * (int)sizeof(R));
+  GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.W = W;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.sA = sA; g.sB = sB; g.sC = sC; g.batch = batch; g.beta = beta;
+  g.mt = (int)((M + C_::BM - 1) / C_::BM);
+  g.nt = (int)((N + C_::BN - 1) / C_::BN);
+  const int64_t tiles = (int64_t)g.mt * g.nt * batch;
+  int splits = choose_splits(tiles, K, C_::BK);
+  const size_t need = (size_t)splits * batch * M * N * EW * sizeof(R);
+  if (splits > 1 && (W == nullptr || wsb < need)) splits = 1;
+  g.splits = splits;
+  g.kchunk = ((K + splits - 1) / splits + C_::BK - 1) / C_::BK * C_::BK;
+  auto aligned = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  g.vecA = aligned(A) && lda % VE == 0 && (batch == 1 || sA % VE == 0);
+  g.vecB = aligned(B) && ldb % VE == 0 && (batch == 1 || sB % VE == 0);
+  if ((int64_t)g.mt * g.nt > INT32_MAX || batch * splits > 65535) {
+    set_error("gemm: grid too large");
+    return TQ_ERR_UNSUPPORTED;
+  }
+  dim3 grid(g.mt * g.nt, 1, (unsigned)(batch * splits));
+#define TQ_GEMM_CASE(ta, tb)                                                              \
+  if (transA == ta && transB == tb) {                                                     \
+    hipLaunchKernelGGL((gemm_kernel<R, CPLX, ta, tb>), grid, dim3(kThreads), 0, stream, g); \
+  }
+  TQ_GEMM_CASE(0, 0)
+  TQ_GEMM_CASE(0, 1)
+  TQ_GEMM_CASE(1, 0)
+  TQ_GEMM_CASE(1, 1)
+#undef TQ_GEMM_CASE
+  TQ_HIP(hipGetLastError());
+  if (splits > 1) {
+    const int64_t total = batch * M * N * EW;
+    const int blocks = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 4096);
+    hipLaunchKernelGGL((splitk_reduce_kernel<R>), dim3(blocks), dim3(kThreads), 0, stream,
+                       (const R*)W, (R*)C, M, N, ldc, sC, batch, splits, EW, (R)beta);
+    TQ_HIP(hipGetLastError());
+  }
+  return TQ_OK;
+}
+
+}  // namespace
+
+size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  int64_t bm, bk;
+  if (dtype == TQ_F32 || dtype == TQ_C64) { bm = Cfg<float>::BM; bk = Cfg<float>::BK; }
+  else { bm = Cfg<double>::BM; bk = Cfg<double>::BK; }
+  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm) * batch;
+  const int s = choose_splits(tiles, K, (int)bk);
+  if (s <= 1) return 0;
+  return (size_t)s * batch * M * N * dtype_size(dtype);
+}
+
+int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
+                const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
+                int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
+                void* workspace, size_t ws_bytes, hipStream_t stream) {
+  TQ_CHECK_ARG(dtype_valid(dtype), "dtype");
+  TQ_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "negative size");
+  TQ_CHECK_ARG(transA == 0 || transA == 1, "transA");
+  TQ_CHECK_ARG(transB == 0 || transB == 1, "transB");
+  if (M == 0 || N == 0 || batch == 0) return TQ_OK;
+  TQ_CHECK_ARG(ldc >= N, "ldc < N");
+  TQ_CHECK_ARG(transA ? lda >= M : lda >= K, "lda");
+  TQ_CHECK_ARG(transB ? ldb >= K : ldb >= N, "ldb");
+  switch (dtype) {
+    case TQ_F32:
+      return launch_typed<float, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+    case TQ_C64:
+      return launch_typed<float, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
+                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+    case TQ_F64:
+      return launch_typed<double, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
+                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+    case TQ_C128:
+      return launch_typed<double, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+  }
+  return TQ_ERR_INVALID;
+}
+
+}  // namespace tq

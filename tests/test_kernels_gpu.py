@@ -1,0 +1,132 @@
+"""HIP kernel parity on the GPU: permute (bit-exact), MFMA GEMM and pairwise contraction
+(tolerance vs a float64/complex128 numpy product of the same operands)."""
+import itertools
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = ["float32", "float64", "complex64", "complex128"]
+# relative tolerance vs an exact (f64/c128) reference, scaled by sqrt(K)
+TOL = {"float32": 2e-6, "complex64": 2e-6, "float64": 1e-14, "complex128": 1e-14}
+
+
+def _rand(rng, shape, dt):
+    x = rng.standard_normal(shape)
+    if dt.startswith("complex"):
+        x = x + 1j * rng.standard_normal(shape)
+    return x.astype(dt)
+
+
+@pytest.fixture(scope="module")
+def T(dev):
+    import torch
+    import tneq_qc_amd.ops as ops  # noqa: F401
+    return torch
+
+
+def _to(T, dev, a):
+    return T.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_permute_binary_legs(T, dev, dt):
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(1)
+    for rank in (1, 3, 7, 12, 16, 20):
+        x = _rand(rng, (2,) * rank, dt)
+        xd = _to(T, dev, x)
+        for _ in range(4):
+            p = rng.permutation(rank)
+            y = ops.permute(xd, list(p)).cpu().numpy()
+            assert np.array_equal(y, np.transpose(x, p)), (rank, p)
+
+
+@pytest.mark.parametrize("dt", ["complex64", "float64"])
+def test_permute_mixed_extents_and_views(T, dev, dt):
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(2)
+    shapes = [(3, 5, 7), (64, 33), (1, 4, 1, 9, 2), (128, 2, 2, 130), (5,), (1,), (17, 1, 4096)]
+    for s in shapes:
+        x = _rand(rng, s, dt)
+        xd = _to(T, dev, x)
+        for p in list(itertools.permutations(range(len(s))))[:6]:
+            y = ops.permute(xd, p).cpu().numpy()
+            assert np.array_equal(y, np.transpose(x, p)), (s, p)
+    # a sliced (strided) view: fix index 1 of the middle leg
+    x = _rand(rng, (2,) * 14, dt)
+    xd = _to(T, dev, x)
+    v = xd[:, :, 1]
+    y = ops.permute(v, list(range(v.ndim))[::-1]).cpu().numpy()
+    assert np.array_equal(y, np.transpose(x[:, :, 1], list(range(13))[::-1]))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_shapes(T, dev, dt, ta, tb):
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(3)
+    exact = "complex128" if dt.startswith("complex") else "float64"
+    for (M, N, K, B) in [(1, 1, 1, 1), (4, 4, 4, 3), (33, 65, 17, 2), (128, 128, 16, 1),
+                         (200, 70, 300, 1), (64, 256, 4096, 1), (3, 300, 2, 5)]:
+        a = _rand(rng, (B, K, M) if ta else (B, M, K), dt)
+        b = _rand(rng, (B, N, K) if tb else (B, K, N), dt)
+        c = ops.gemm(_to(T, dev, a), _to(T, dev, b), bool(ta), bool(tb)).cpu().numpy()
+        ae = a.astype(exact)
+        be = b.astype(exact)
+        ref = np.matmul(np.swapaxes(ae, 1, 2) if ta else ae, np.swapaxes(be, 1, 2) if tb else be)
+        err = np.abs(c - ref).max() / max(1e-30, np.abs(ref).max())
+        assert err < TOL[dt] * np.sqrt(K) * 10, (M, N, K, B, err)
+
+
+def test_gemm_beta_and_splitk(T, dev):
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(4)
+    a = _rand(rng, (256, 8192), "complex64")
+    b = _rand(rng, (8192, 128), "complex64")
+    c0 = _rand(rng, (1, 256, 128), "complex64")
+    cd = _to(T, dev, c0)
+    ops.gemm(_to(T, dev, a), _to(T, dev, b), out=cd, beta=1.0)
+    ref = a.astype("complex128") @ b.astype("complex128") + c0[0]
+    err = np.abs(cd.cpu().numpy()[0] - ref).max() / np.abs(ref).max()
+    assert err < 1e-5
+
+
+@pytest.mark.parametrize("dt", ["complex64", "complex128", "float32"])
+def test_contract_pair_random(T, dev, dt):
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(5)
+    exact = "complex128" if dt.startswith("complex") else "float64"
+    for trial in range(30):
+        nmodes = rng.integers(2, 9)
+        ext = {m: int(rng.integers(1, 4)) for m in range(nmodes)}
+        ma = list(rng.choice(nmodes, size=rng.integers(1, nmodes + 1), replace=False))
+        mb = list(rng.choice(nmodes, size=rng.integers(1, nmodes + 1), replace=False))
+        allm = sorted(set(ma) | set(mb))
+        mc = [m for m in allm if rng.random() < 0.5]
+        rng.shuffle(mc)
+        a = _rand(rng, [ext[m] for m in ma], dt)
+        b = _rand(rng, [ext[m] for m in mb], dt)
+        c = ops.contract_pair(ma, _to(T, dev, a), mb, _to(T, dev, b), mc).cpu().numpy()
+        L = "abcdefghij"
+        eq = "".join(L[m] for m in ma) + "," + "".join(L[m] for m in mb) + "->" + "".join(L[m] for m in mc)
+        ref = np.einsum(eq, a.astype(exact), b.astype(exact))
+        scale = max(1.0, np.abs(ref).max())
+        tol = 1e-12 if dt == "complex128" else 1e-4
+        assert np.abs(c - ref).max() / scale < tol, (eq, trial)
+
+
+def test_contract_pair_gate_apply(T, dev):
+    """(2,)*20 state absorbing a (2,2,2,2) gate on two adjacent legs -> the APPLY lowering."""
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(6)
+    s = _rand(rng, (2,) * 20, "complex64")
+    g = _rand(rng, (2, 2, 2, 2), "complex64")
+    ma = list(range(20))
+    mg = [7, 8, 100, 101]
+    mc = ma[:7] + [100, 101] + ma[9:]
+    c = ops.contract_pair(ma, _to(T, dev, s), mg, _to(T, dev, g), mc).cpu().numpy()
+    ref = np.moveaxis(np.tensordot(s.astype("complex128"), g.astype("complex128"), axes=([7, 8], [0, 1])),
+                      [18, 19], [7, 8])
+    assert np.abs(c - ref).max() / np.abs(ref).max() < 1e-5
