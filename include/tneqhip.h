@@ -104,8 +104,10 @@ int tq_plan_create(tq_plan* plan, int dtype, int n_inputs, const int32_t* in_ran
                    int out_rank, const int32_t* out_modes, int n_steps, const int32_t* path,
                    int n_sliced, const int32_t* sliced_modes);
 
-/* Queries: key = "n_slices", "arena_bytes", "flops" (per slice, algorithmic), "bytes_moved",
- * "n_kernels" (launches per slice), "n_gemm", "n_apply", "n_permute".  Returns -1 if unknown. */
+/* Queries (algorithmic counts): "n_slices", "arena_bytes", "table_bytes", "out_numel",
+ * "flops" / "bytes_moved" (a whole execute over all slices), "flops_once" / "bytes_once"
+ * (slice-invariant part, hoisted: run once per execute), "flops_slice" / "bytes_slice"
+ * (per slice), "n_kernels", "n_ops_once", "n_gemm", "n_apply", "n_permute".  -1 if unknown. */
 int64_t tq_plan_query(tq_plan plan, const char* key);
 /* human-readable per-step description into buf (for debugging / DESIGN evidence) */
 int tq_plan_describe(tq_plan plan, char* buf, size_t n);
@@ -115,6 +117,17 @@ int tq_plan_describe(tq_plan plan, char* buf, size_t n);
 int tq_plan_execute(tq_plan plan, const void* const* inputs, void* out, int64_t slice_begin,
                     int64_t slice_end, int64_t slice_step, int accumulate, void* stream);
 int tq_plan_destroy(tq_plan plan);
+
+/* Per-op timing with HIP events recorded on the execution stream around every kernel of the
+ * plan (bench evidence for the roofline of the dominant kernel).  tq_plan_profile(plan, mask)
+ * resets the records and times the op kinds whose bit (1 << kind) is set in mask (-1 = all,
+ * 0 = off).  tq_plan_profile_read sums, over the launches of one
+ * op kind since the reset (TQ_OP_PERMUTE / TQ_OP_GEMM / TQ_OP_APPLY, or -1 for all), the
+ * elapsed milliseconds, the launch count and the algorithmic flops / bytes. */
+enum { TQ_OP_PERMUTE = 0, TQ_OP_GEMM = 1, TQ_OP_APPLY = 2, TQ_OP_AXPY = 3 };
+int tq_plan_profile(tq_plan plan, int enable);
+int tq_plan_profile_read(tq_plan plan, int op_kind, double* total_ms, int64_t* launches,
+                         double* flops, double* bytes);
 
 #ifdef __cplusplus
 }

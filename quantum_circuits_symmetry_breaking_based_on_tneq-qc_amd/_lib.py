@@ -22,7 +22,9 @@ EXPORTED = (
     "tq_version", "tq_last_error", "tq_device_synchronize", "tq_permute", "tq_gemm_batched",
     "tq_gemm_workspace_size", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
     "tq_plan_create", "tq_plan_query", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
+    "tq_plan_profile", "tq_plan_profile_read",
 )
+TQ_OP_PERMUTE, TQ_OP_GEMM, TQ_OP_APPLY, TQ_OP_AXPY = 0, 1, 2, 3
 
 
 class TneqHipError(RuntimeError):
@@ -59,6 +61,9 @@ _SIGS = {
     "tq_plan_execute": (_c.c_int, [_vp, _c.POINTER(_vp), _vp, _c.c_int64, _c.c_int64, _c.c_int64,
                                    _c.c_int, _vp]),
     "tq_plan_destroy": (_c.c_int, [_vp]),
+    "tq_plan_profile": (_c.c_int, [_vp, _c.c_int]),
+    "tq_plan_profile_read": (_c.c_int, [_vp, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64),
+                                        _c.POINTER(_c.c_double), _c.POINTER(_c.c_double)]),
 }
 
 

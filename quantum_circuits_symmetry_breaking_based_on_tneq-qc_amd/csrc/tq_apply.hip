@@ -4,8 +4,9 @@
 // (a (2,2,2,2) gate, a (2,) input state or output projector) into a large running tensor
 // (reference: each such step is a tensordot inside the opt_einsum ContractExpression built at
 // tneq_qc/contractor/einsum_strategy.py:639-643, i.e. transpose + GEMM with K <= 4).
-// When the contracted modes of the big operand S are adjacent in its layout, the step is
-//      C[o][n][i] = sum_k S[o][k][i] * G[k][n]
+// When the contracted modes of the big operand S form at most two runs in its layout,
+// S = [O][K1][M][K2][I], the step is
+//      C[o][n][m][i] = sum_{k1,k2} S[o][k1][m][k2][i] * G[k1 k2][n]
 // (a strided batched GEMM with tiny K, N): no transpose is needed and the step is purely
 // HBM-bound, so it is done as one streaming pass: read S once, write C once
 // (algorithmic bytes = (numel(S) + numel(C)) * sizeof).  G lives in LDS.
@@ -21,20 +22,32 @@ constexpr int kThreads = 256;
 
 template <typename T, int KMAX, int NMAX>
 __global__ void __launch_bounds__(kThreads)
-apply_kernel(const T* __restrict__ S, const T* __restrict__ G, T* __restrict__ C, int64_t O,
-             int K, int N, int64_t I, float beta_f, double beta_d, int use_beta) {
+apply_kernel(const T* __restrict__ S, const T* __restrict__ G, const int32_t* __restrict__ gidx,
+             T* __restrict__ C, int64_t O,
+             int K1, int64_t M, int K2, int64_t I, int N, float beta_f, double beta_d,
+             int use_beta) {
   __shared__ T g[KMAX * NMAX];
-  for (int t = threadIdx.x; t < K * N; t += kThreads) g[t] = G[t];
+  __shared__ int64_t koff[KMAX];
+  const int K = K1 * K2;
+  const int64_t MI = M * I;
+  const int64_t total = O * MI;
+  const int64_t sK1 = M * K2 * I, sK2 = I;  // strides of the two contracted runs in S
+  for (int t = threadIdx.x; t < K * N; t += kThreads) g[t] = G[gidx ? gidx[t] : t];
+  for (int k = threadIdx.x; k < KMAX; k += kThreads) koff[k] = (k / K2) * sK1 + (k % K2) * sK2;
   __syncthreads();
-  const int64_t total = O * I;
   for (int64_t x = blockIdx.x * (int64_t)kThreads + threadIdx.x; x < total;
        x += (int64_t)gridDim.x * kThreads) {
-    const int64_t o = x / I, i = x - o * I;
-    const T* s = S + o * K * I + i;
+    int64_t o, r, m, i;
+    if (M == 1) {  // one contracted run: skip the middle split
+      o = x / I; i = x - o * I; m = 0; r = i;
+    } else {
+      o = x / MI; r = x - o * MI; m = r / I; i = r - m * I;
+    }
+    const T* s = S + o * K1 * sK1 + m * K2 * I + i;
     T v[KMAX];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) v[k] = k < K ? s[k * I] : tzero<T>();
-    T* c = C + o * N * I + i;
+    for (int k = 0; k < KMAX; ++k) v[k] = k < K ? s[koff[k]] : tzero<T>();
+    T* c = C + o * N * MI + r;
 #pragma unroll
     for (int n = 0; n < NMAX; ++n) {
       if (n < N) {
@@ -43,10 +56,10 @@ apply_kernel(const T* __restrict__ S, const T* __restrict__ G, T* __restrict__ C
         for (int k = 0; k < KMAX; ++k)
           if (k < K) cmac(acc, v[k], g[k * N + n]);
         if (use_beta) {
-          if constexpr (sizeof(typename Traits<T>::R) == 4) acc = acc + c[n * I] * beta_f;
-          else acc = acc + c[n * I] * beta_d;
+          if constexpr (sizeof(typename Traits<T>::R) == 4) acc = acc + c[n * MI] * beta_f;
+          else acc = acc + c[n * MI] * beta_d;
         }
-        c[n * I] = acc;
+        c[n * MI] = acc;
       }
     }
   }
@@ -67,20 +80,23 @@ axpy_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ y, float bf, dou
 }
 
 template <typename T>
-int apply_t(int64_t O, int64_t K, int64_t N, int64_t I, const void* S, const void* G, void* C,
-            double beta, hipStream_t stream) {
-  const int64_t total = O * I;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + kThreads - 1) / kThreads, 4096));
+int apply_t(int64_t O, int64_t K1, int64_t M, int64_t K2, int64_t I, int64_t N, const void* S,
+            const void* G, const int32_t* gidx, void* C, double beta, hipStream_t stream) {
+  const int64_t total = O * M * I;
+  const int64_t K = K1 * K2;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + kThreads - 1) / kThreads, 8192));
   const int ub = beta != 0.0;
 #define TQ_APPLY_CASE(KM, NM)                                                                 \
   if (K <= KM && N <= NM) {                                                                   \
     hipLaunchKernelGGL((apply_kernel<T, KM, NM>), dim3(blocks), dim3(kThreads), 0, stream,    \
-                       (const T*)S, (const T*)G, (T*)C, O, (int)K, (int)N, I, (float)beta,   \
-                       beta, ub);                                                             \
+                       (const T*)S, (const T*)G, gidx, (T*)C, O, (int)K1, M, (int)K2, I,     \
+                       (int)N,                                                                \
+                       (float)beta, beta, ub);                                                \
     TQ_HIP(hipGetLastError());                                                                \
     return TQ_OK;                                                                             \
   }
   TQ_APPLY_CASE(2, 1)
+  TQ_APPLY_CASE(2, 2)
   TQ_APPLY_CASE(4, 4)
   TQ_APPLY_CASE(4, 16)
   TQ_APPLY_CASE(16, 4)
@@ -102,14 +118,15 @@ int axpy_t(int64_t n, const void* x, void* y, double beta, hipStream_t stream) {
 
 }  // namespace
 
-int apply_launch(int dtype, int64_t O, int64_t K, int64_t N, int64_t I, const void* S,
-                 const void* G, void* C, double beta, hipStream_t stream) {
-  if (O * I == 0) return TQ_OK;
+int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_t I, int64_t N,
+                 const void* S, const void* G, const int32_t* gidx, void* C, double beta,
+                 hipStream_t stream) {
+  if (O * M * I == 0) return TQ_OK;
   switch (dtype) {
-    case TQ_F32: return apply_t<float>(O, K, N, I, S, G, C, beta, stream);
-    case TQ_F64: return apply_t<double>(O, K, N, I, S, G, C, beta, stream);
-    case TQ_C64: return apply_t<c64>(O, K, N, I, S, G, C, beta, stream);
-    case TQ_C128: return apply_t<c128>(O, K, N, I, S, G, C, beta, stream);
+    case TQ_F32: return apply_t<float>(O, K1, M, K2, I, N, S, G, gidx, C, beta, stream);
+    case TQ_F64: return apply_t<double>(O, K1, M, K2, I, N, S, G, gidx, C, beta, stream);
+    case TQ_C64: return apply_t<c64>(O, K1, M, K2, I, N, S, G, gidx, C, beta, stream);
+    case TQ_C128: return apply_t<c128>(O, K1, M, K2, I, N, S, G, gidx, C, beta, stream);
   }
   set_error("apply: bad dtype");
   return TQ_ERR_INVALID;

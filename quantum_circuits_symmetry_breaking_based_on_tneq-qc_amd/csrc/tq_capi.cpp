@@ -156,6 +156,11 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "table_bytes") return (int64_t)P.table_bytes;
   if (k == "flops") return (int64_t)P.flops;
   if (k == "bytes_moved") return (int64_t)P.bytes;
+  if (k == "flops_once") return (int64_t)P.flops_once;
+  if (k == "flops_slice") return (int64_t)P.flops_slice;
+  if (k == "bytes_once") return (int64_t)P.bytes_once;
+  if (k == "bytes_slice") return (int64_t)P.bytes_slice;
+  if (k == "n_ops_once") { int64_t c = 0; for (auto& o : P.ops) c += o.invariant; return c; }
   if (k == "n_kernels") return (int64_t)P.ops.size();
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;
@@ -185,6 +190,25 @@ int tq_plan_execute(tq_plan p, const void* const* inputs, void* out, int64_t sli
   }
   return tq::plan_run(p->plan, inputs, out, slice_begin, slice_end, slice_step, accumulate,
                       (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+int tq_plan_profile(tq_plan p, int enable) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(p != nullptr, "null plan");
+  tq::Plan& P = p->plan;
+  for (auto& ev : P.ev_used) P.ev_free.push_back(ev);  // reset: recycle recorded events
+  P.ev_used.clear();
+  P.profile = (unsigned)enable;
+  return TQ_OK;
+  TQ_GUARD_END
+}
+
+int tq_plan_profile_read(tq_plan p, int op_kind, double* total_ms, int64_t* launches,
+                         double* flops, double* bytes) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(p != nullptr, "null plan");
+  return tq::plan_profile_read(p->plan, op_kind, total_ms, launches, flops, bytes);
   TQ_GUARD_END
 }
 

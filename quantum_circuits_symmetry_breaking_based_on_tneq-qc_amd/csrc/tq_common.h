@@ -96,10 +96,11 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
                 void* workspace, size_t ws_bytes, hipStream_t stream);
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
-// apply a small operand along a contiguous mode group (tq_apply.hip):
-//   C[o][n][i] = sum_k S[o][k][i] * G[k][n]     (S, C contiguous; G contiguous K x N)
-int apply_launch(int dtype, int64_t O, int64_t K, int64_t N, int64_t I, const void* S,
-                 const void* G, void* C, double beta, hipStream_t stream);
+// apply a small operand along (at most two runs of) contracted modes (tq_apply.hip):
+//   C[o][n][m][i] = sum_{k1,k2} S[o][k1][m][k2][i] * G[k1*K2+k2][n]   (S, C, G contiguous)
+int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_t I, int64_t N,
+                 const void* S, const void* G, const int32_t* gidx, void* C, double beta,
+                 hipStream_t stream);
 int axpy_launch(int dtype, int64_t n, const void* x, void* y, double beta, hipStream_t stream);
 
 }  // namespace tq

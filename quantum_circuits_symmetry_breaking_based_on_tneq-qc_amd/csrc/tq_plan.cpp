@@ -6,8 +6,9 @@
 //   * walks the SSA pairwise path, tracks which modes are still needed (mode reference counts),
 //     classifies every mode of each pair (batch / contracted / free / single-side sum),
 //   * picks per step the cheapest lowering:
-//       APPLY  one operand small and its contracted modes adjacent in the big operand
-//              -> one streaming pass, no transpose (tq_apply.hip);
+//       APPLY  one operand small (<= 32 x 32) and its contracted modes forming at most two runs
+//              in the big operand -> one streaming pass, no transpose (tq_apply.hip); the small
+//              operand is read in any layout through a gather table (no extra launch);
 //       GEMM   TTGT: reuse any operand whose layout is already [batch][M][K] / [batch][K][M]
 //              (no transpose), otherwise permute it (tq_permute.hip); operand roles and the
 //              K order are chosen to minimise transposed bytes; MFMA GEMM (tq_gemm.hip);
@@ -19,6 +20,7 @@
 #include "tq_plan.h"
 
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <numeric>
 #include <set>
@@ -43,6 +45,7 @@ struct Live {
   std::vector<int64_t> stride;
   BufRef buf;
   bool owned = false;  // arena intermediate that must be freed after use
+  bool dep = false;    // depends on a sliced input (otherwise computed once per execute)
   int64_t numel() const { return prod(ext); }
   bool contiguous() const {
     auto cs = contig_strides(ext);
@@ -132,6 +135,7 @@ class Compiler {
       cur += in_ranks[i];
       L.modes = v.modes; L.ext = v.ext; L.stride = v.stride;
       L.buf.kind = BUF_INPUT; L.buf.index = i; L.buf.off = 0;
+      for (int64_t ss : v.slice_stride) L.dep |= ss != 0;
       P_.inputs.push_back(v);
       live_.push_back(L);
     }
@@ -154,6 +158,23 @@ class Compiler {
     // reference counts: live tensors + output
     for (auto& L : live_) for (int m : L.modes) cnt_[m]++;
     for (int m : P_.out_modes) cnt_[m]++;
+    // ---- pre-pass: which SSA ids depend on a sliced input, and which slice-invariant results
+    // are read by slice-dependent steps (those are "pinned": kept in a region of their own that
+    // no slice-dependent buffer ever reuses, since invariant ops do not re-run per slice)
+    {
+      std::vector<char> dep(n_inputs + n_steps, 0);
+      for (int i = 0; i < n_inputs; ++i) dep[i] = live_[i].dep;
+      pinned_.assign(n_inputs + n_steps, 0);
+      for (int s = 0; s < n_steps; ++s) {
+        const int x = path[2 * s], y = path[2 * s + 1];
+        if (x < 0 || y < 0 || x >= n_inputs + s || y >= n_inputs + s) break;  // checked below
+        dep[n_inputs + s] = dep[x] || dep[y];
+        if (dep[n_inputs + s]) {
+          if (!dep[x] && x >= n_inputs) pinned_[x] = 1;
+          if (!dep[y] && y >= n_inputs) pinned_[y] = 1;
+        }
+      }
+    }
     // ---- steps
     std::vector<bool> used(n_inputs + n_steps, false);
     for (int s = 0; s < n_steps; ++s) {
@@ -163,6 +184,7 @@ class Compiler {
       TQ_CHECK_ARG(!used[x] && !used[y], "path uses a tensor twice");
       used[x] = used[y] = true;
       Live res;
+      pin_next_ = pinned_[nid];
       TQ_TRY(step(s, live_[x], live_[y], s == n_steps - 1, res));
       live_.push_back(res);
     }
@@ -176,7 +198,8 @@ class Compiler {
         TQ_CHECK_ARG(outset.count(m), "single-input trace/sum is unsupported");
       TQ_TRY(emit_permute(L, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, -1, "copy->out"));
     }
-    P_.arena_bytes = (size_t)arena_.peak();
+    P_.pinned_base = (size_t)((arena_.peak() + kAlign - 1) / kAlign * kAlign);
+    P_.arena_bytes = P_.pinned_base + (size_t)pinned_arena_.peak();
     // table layout
     size_t tb = 0;
     P_.perm_tab_off.clear();
@@ -184,16 +207,24 @@ class Compiler {
       P_.perm_tab_off.push_back(tb);
       tb += (perm_plan_table_bytes(pp) + kAlign - 1) / kAlign * kAlign;
     }
+    P_.gtab_off.clear();
+    for (auto& g : P_.gtabs) {
+      P_.gtab_off.push_back(tb);
+      tb += (g.size() * sizeof(int32_t) + kAlign - 1) / kAlign * kAlign;
+    }
     P_.table_bytes = tb;
     for (auto& op : P_.ops) {
-      P_.flops += op.flops;
-      P_.bytes += op.bytes;
+      (op.invariant ? P_.flops_once : P_.flops_slice) += op.flops;
+      (op.invariant ? P_.bytes_once : P_.bytes_slice) += op.bytes;
       P_.n_gemm += op.kind == OP_GEMM;
       P_.n_apply += op.kind == OP_APPLY;
       P_.n_permute += op.kind == OP_PERMUTE;
     }
+    P_.flops = P_.flops_once + P_.flops_slice * (double)P_.n_slices;
+    P_.bytes = P_.bytes_once + P_.bytes_slice * (double)P_.n_slices;
     std::ostringstream d;
-    for (size_t i = 0; i < P_.ops.size(); ++i) d << P_.ops[i].note << "\n";
+    for (size_t i = 0; i < P_.ops.size(); ++i)
+      d << (P_.ops[i].invariant ? "[once]  " : "[slice] ") << P_.ops[i].note << "\n";
     P_.describe = d.str();
     return TQ_OK;
   }
@@ -218,7 +249,17 @@ class Compiler {
     return b;
   }
   void release(const Live& L) {
-    if (L.owned) arena_.release(L.buf.off * (int64_t)P_.esz);
+    if (L.owned && L.buf.kind == BUF_ARENA) arena_.release(L.buf.off * (int64_t)P_.esz);
+  }
+  // the step result's buffer: pinned results live in the separate pinned region
+  BufRef new_result_buf(int64_t numel, int64_t* off_out) {
+    if (!pin_next_) return new_buf(numel, off_out);
+    const int64_t off = pinned_arena_.alloc(numel * (int64_t)P_.esz);
+    *off_out = off;
+    BufRef b;
+    b.kind = BUF_PINNED;
+    b.off = off / (int64_t)P_.esz;
+    return b;
   }
 
   // permute X into contiguous `order` (+ broadcast modes `bcast` with stride 0) at dst
@@ -288,13 +329,18 @@ class Compiler {
     }
     for (int m : B0.modes) if (!inA.count(m)) (cnt_[m] > 0 ? freeB : sumB).insert(m);
 
+    const size_t first_op = P_.ops.size();
     int rc = TQ_OK;
     const bool applied = try_apply(s, A0, B0, final, batch, contr, sumA, sumB, res, rc);
     if (rc != TQ_OK) return rc;
     if (!applied) TQ_TRY(gemm_step(s, A0, B0, final, batch, contr, freeA, freeB, sumA, sumB, res));
     for (int m : res.modes) cnt_[m]++;
-    release(A0);
-    release(B0);
+    // slice-invariant hoisting: a step that reads no sliced input runs once per execute; its
+    // result is pinned in the arena when a slice-dependent step consumes it
+    res.dep = A0.dep || B0.dep;
+    for (size_t k = first_op; k < P_.ops.size(); ++k) P_.ops[k].invariant = !res.dep;
+    if (!(res.dep && !A0.dep)) release(A0);
+    if (!(res.dep && !B0.dep)) release(B0);
     return TQ_OK;
   }
 
@@ -304,7 +350,7 @@ class Compiler {
                        int64_t* off) {
     *direct = final && order == P_.out_modes;
     if (*direct) { *off = -1; return BufRef{BUF_OUTPUT, 0, 0}; }
-    return new_buf(numel, off);
+    return new_result_buf(numel, off);
   }
 
   bool try_apply(int s, const Live& A0, const Live& B0, bool final, const std::set<int>& batch,
@@ -318,52 +364,74 @@ class Compiler {
     const int64_t K = ext_of(std::vector<int>(contr.begin(), contr.end()));
     const int64_t N = Sm.numel() / K;
     if (Sm.numel() > 1024 || K > 32 || N > 32) return false;
-    // contracted modes adjacent in the big operand
-    int p = -1;
-    for (size_t i = 0; i < Bg.modes.size(); ++i)
-      if (contr.count(Bg.modes[i])) { p = (int)i; break; }
-    const int c = (int)contr.size();
-    for (int i = p; i < p + c; ++i)
-      if (i >= (int)Bg.modes.size() || !contr.count(Bg.modes[i])) return false;
-    std::vector<int> korder(Bg.modes.begin() + p, Bg.modes.begin() + p + c);
+    // contracted modes must form at most two runs in the big operand: [O][K1][M][K2][I]
+    std::vector<std::pair<int, int>> runs;  // (start, length)
+    for (int i = 0; i < (int)Bg.modes.size(); ++i) {
+      if (!contr.count(Bg.modes[i])) continue;
+      if (!runs.empty() && runs.back().first + runs.back().second == i) runs.back().second++;
+      else runs.push_back({i, 1});
+    }
+    if (runs.empty() || runs.size() > 2) return false;
+    const int p1 = runs[0].first, c1 = runs[0].second;
+    const int p2 = runs.size() == 2 ? runs[1].first : p1 + c1;
+    const int c2 = runs.size() == 2 ? runs[1].second : 0;
+    std::vector<int> korder(Bg.modes.begin() + p1, Bg.modes.begin() + p1 + c1);
+    korder.insert(korder.end(), Bg.modes.begin() + p2, Bg.modes.begin() + p2 + c2);
     std::vector<int> nfree;
     for (int m : Sm.modes) if (!contr.count(m)) nfree.push_back(m);
-    // small operand as G[K][N]
-    std::vector<int> gorder = korder;
-    gorder.insert(gorder.end(), nfree.begin(), nfree.end());
-    BufRef gbuf = Sm.buf;
-    int64_t goff = -1;
-    if (!(Sm.contiguous() && Sm.modes == gorder)) {
-      gbuf = new_buf(Sm.numel(), &goff);
-      rc = emit_permute(Sm, gorder, {}, gbuf, false, s, "small->[K][N]");
-      if (rc != TQ_OK) return true;
+    // small operand read as G[K][N] through a gather table (any layout / strides, no launch)
+    int gtab = -1;
+    {
+      std::vector<int> gorder = korder;
+      gorder.insert(gorder.end(), nfree.begin(), nfree.end());
+      if (!(Sm.contiguous() && Sm.modes == gorder)) {
+        std::vector<int64_t> gext, gst;
+        for (int m : gorder) {
+          const int p = Sm.pos(m);
+          gext.push_back(Sm.ext[p]);
+          gst.push_back(Sm.stride[p]);
+        }
+        const int64_t n = prod(gext);
+        std::vector<int32_t> tab(n);
+        for (int64_t t = 0; t < n; ++t) {
+          int64_t rem = t, off = 0;
+          for (int d = (int)gext.size() - 1; d >= 0; --d) { off += (rem % gext[d]) * gst[d]; rem /= gext[d]; }
+          tab[t] = (int32_t)off;
+        }
+        gtab = (int)P_.gtabs.size();
+        P_.gtabs.push_back(std::move(tab));
+      }
     }
-    std::vector<int> order(Bg.modes.begin(), Bg.modes.begin() + p);
+    std::vector<int> order(Bg.modes.begin(), Bg.modes.begin() + p1);
     order.insert(order.end(), nfree.begin(), nfree.end());
-    order.insert(order.end(), Bg.modes.begin() + p + c, Bg.modes.end());
-    int64_t O = 1, I = 1;
-    for (int i = 0; i < p; ++i) O *= Bg.ext[i];
-    for (size_t i = p + c; i < Bg.modes.size(); ++i) I *= Bg.ext[i];
-    const int64_t outn = O * N * I;
+    order.insert(order.end(), Bg.modes.begin() + p1 + c1, Bg.modes.begin() + p2);
+    order.insert(order.end(), Bg.modes.begin() + p2 + c2, Bg.modes.end());
+    int64_t O = 1, K1 = 1, M = 1, K2 = 1, I = 1;
+    for (int i = 0; i < p1; ++i) O *= Bg.ext[i];
+    for (int i = p1; i < p1 + c1; ++i) K1 *= Bg.ext[i];
+    for (int i = p1 + c1; i < p2; ++i) M *= Bg.ext[i];
+    for (int i = p2; i < p2 + c2; ++i) K2 *= Bg.ext[i];
+    for (size_t i = p2 + c2; i < Bg.modes.size(); ++i) I *= Bg.ext[i];
+    const int64_t outn = O * N * M * I;
     bool direct;
     int64_t roff;
     BufRef tgt = result_target(final, order, outn, &direct, &roff);
     Op op;
     op.kind = OP_APPLY;
     op.a = Bg.buf;
-    op.b = gbuf;
+    op.b = Sm.buf;
+    op.gtab = gtab;
     op.c = tgt;
     op.writes_output = direct;
-    op.O = O; op.K = K; op.N = N; op.I = I;
+    op.O = O; op.K = K1; op.M = M; op.K2 = K2; op.N = N; op.I = I;
     op.step = s;
-    op.flops = (double)O * I * K * N * (cplx_ ? 8.0 : 2.0);
-    op.bytes = (double)(O * K * I + outn + K * N) * P_.esz;
+    op.flops = (double)O * M * I * K * N * (cplx_ ? 8.0 : 2.0);
+    op.bytes = (double)(O * K * M * I + outn + K * N) * P_.esz;
     std::ostringstream o;
-    o << "step " << s << " APPLY O=" << O << " K=" << K << " N=" << N << " I=" << I
-      << (direct ? " ->OUT" : "");
+    o << "step " << s << " APPLY O=" << O << " K1=" << K1 << " M=" << M << " K2=" << K2
+      << " I=" << I << " N=" << N << (direct ? " ->OUT" : "");
     op.note = o.str();
     P_.ops.push_back(op);
-    if (goff >= 0) arena_.release(goff);
     res.modes = order;
     for (int m : order) res.ext.push_back(ext_[m]);
     res.stride = contig_strides(res.ext);
@@ -513,6 +581,9 @@ class Compiler {
   std::map<int, int64_t> ext_;
   std::map<int, int> cnt_;
   Arena arena_;
+  Arena pinned_arena_;
+  std::vector<char> pinned_;
+  bool pin_next_ = false;
 };
 
 }  // namespace
@@ -547,13 +618,37 @@ int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
     std::vector<char> host(P.table_bytes, 0);
     for (size_t i = 0; i < P.perms.size(); ++i)
       if (perm_plan_table_bytes(P.perms[i])) perm_plan_pack_table(P.perms[i], host.data() + P.perm_tab_off[i]);
+    for (size_t i = 0; i < P.gtabs.size(); ++i)
+      std::memcpy(host.data() + P.gtab_off[i], P.gtabs[i].data(), P.gtabs[i].size() * sizeof(int32_t));
     TQ_HIP(hipMemcpyAsync(P.d_tables, host.data(), P.table_bytes, hipMemcpyHostToDevice, stream));
     TQ_HIP(hipStreamSynchronize(stream));
   }
   return TQ_OK;
 }
 
+int plan_profile_read(Plan& P, int kind, double* ms, int64_t* launches, double* flops,
+                      double* bytes) {
+  double t = 0, f = 0, b = 0;
+  int64_t n = 0;
+  for (auto& ev : P.ev_used) {
+    if (kind >= 0 && ev.kind != kind) continue;
+    TQ_HIP(hipEventSynchronize(ev.b));
+    float e = 0;
+    TQ_HIP(hipEventElapsedTime(&e, ev.a, ev.b));
+    t += e; f += ev.flops; b += ev.bytes; ++n;
+  }
+  if (ms) *ms = t;
+  if (launches) *launches = n;
+  if (flops) *flops = f;
+  if (bytes) *bytes = b;
+  return TQ_OK;
+}
+
 void plan_release(Plan& P) {
+  for (auto& ev : P.ev_used) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
+  for (auto& ev : P.ev_free) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
+  P.ev_used.clear();
+  P.ev_free.clear();
   if (P.owns_device) {
     if (P.d_arena) (void)hipFree(P.d_arena);
     if (P.d_tables) (void)hipFree(P.d_tables);
@@ -588,13 +683,28 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
       switch (b.kind) {
         case BUF_INPUT: return (char*)inputs[b.index] + (in_off[b.index] + b.off) * esz;
         case BUF_ARENA: return (char*)P.d_arena + b.off * esz;
+        case BUF_PINNED: return (char*)P.d_arena + P.pinned_base + b.off * esz;
         case BUF_OUTPUT: return (char*)out + b.off * esz;
       }
       return nullptr;
     };
     const double beta_out = first ? 0.0 : 1.0;
     for (const Op& op : P.ops) {
+      if (op.invariant && sl != s_begin) continue;  // hoisted: computed in this call's first slice
       const double beta = op.writes_output ? beta_out : 0.0;
+      Plan::Ev ev{};
+      const bool prof = (P.profile >> op.kind) & 1;
+      if (prof) {
+        if (P.ev_free.empty()) {
+          TQ_HIP(hipEventCreate(&ev.a));
+          TQ_HIP(hipEventCreate(&ev.b));
+        } else {
+          ev = P.ev_free.back();
+          P.ev_free.pop_back();
+        }
+        ev.kind = op.kind; ev.flops = op.flops; ev.bytes = op.bytes;
+        TQ_HIP(hipEventRecord(ev.a, stream));
+      }
       switch (op.kind) {
         case OP_PERMUTE:
           TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm],
@@ -606,12 +716,17 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
                              op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, stream));
           break;
         case OP_APPLY:
-          TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.N, op.I, ptr(op.a), ptr(op.b), ptr(op.c),
-                              beta, stream));
+          TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.M, op.K2, op.I, op.N, ptr(op.a), ptr(op.b),
+                              op.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[op.gtab]) : nullptr,
+                              ptr(op.c), beta, stream));
           break;
         case OP_AXPY:
           TQ_TRY(axpy_launch(P.dtype, op.n, ptr(op.a), ptr(op.c), beta, stream));
           break;
+      }
+      if (prof) {
+        TQ_HIP(hipEventRecord(ev.b, stream));
+        P.ev_used.push_back(ev);
       }
     }
     first = false;

@@ -10,7 +10,7 @@
 namespace tq {
 
 // where an operand lives
-enum BufKind { BUF_INPUT = 0, BUF_ARENA = 1, BUF_OUTPUT = 2, BUF_TABLE = 3 };
+enum BufKind { BUF_INPUT = 0, BUF_ARENA = 1, BUF_OUTPUT = 2, BUF_TABLE = 3, BUF_PINNED = 4 };
 struct BufRef {
   int kind = BUF_ARENA;
   int64_t index = 0;  // input id for BUF_INPUT
@@ -23,6 +23,7 @@ struct Op {
   int kind = OP_PERMUTE;
   BufRef a, b, c;       // permute: a -> c ; gemm: c = a*b ; apply: c = a (x) b ; axpy: c += a
   bool writes_output = false;
+  bool invariant = false;  // reads no sliced input: run once per execute call (hoisted)
   // permute
   int perm = -1;        // index into Plan::perms
   // gemm
@@ -30,8 +31,9 @@ struct Op {
   int64_t M = 0, N = 0, K = 0, batch = 1, lda = 0, ldb = 0, ldc = 0, sA = 0, sB = 0, sC = 0;
   BufRef ws;
   size_t ws_bytes = 0;
-  // apply
-  int64_t O = 0, I = 0;  // with K, N above
+  // apply: S = [O][K][M][K2][I] -> C = [O][N][M][I]   (K, N above)
+  int64_t O = 0, I = 0, K2 = 1;
+  int gtab = -1;         // gather table of the small operand (index into Plan::gtabs)
   // axpy
   int64_t n = 0;
   // bookkeeping
@@ -61,12 +63,21 @@ struct Plan {
   std::vector<Op> ops;
   std::vector<PermPlan> perms;
   std::vector<size_t> perm_tab_off;   // byte offset in the table buffer
+  std::vector<std::vector<int32_t>> gtabs;  // APPLY small-operand gather tables
+  std::vector<size_t> gtab_off;
   size_t table_bytes = 0;
   size_t arena_bytes = 0;
+  size_t pinned_base = 0;             // pinned (hoisted, slice-invariant) results live above this
   void* d_arena = nullptr;
   void* d_tables = nullptr;
   bool owns_device = false;
-  double flops = 0, bytes = 0;
+  // optional per-op-kind timing with HIP events on the execution stream (bench evidence)
+  unsigned profile = 0;  // bit k set: time ops of kind k
+  struct Ev { hipEvent_t a, b; int kind; double flops, bytes; };
+  std::vector<Ev> ev_used, ev_free;
+  double flops = 0, bytes = 0;              // whole execute (all slices)
+  double flops_once = 0, bytes_once = 0;    // slice-invariant (hoisted) part
+  double flops_slice = 0, bytes_slice = 0;  // per slice
   int n_gemm = 0, n_apply = 0, n_permute = 0;
   std::string describe;
 };
@@ -80,5 +91,6 @@ int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream);
 int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
              int64_t s_step, int accumulate, hipStream_t stream);
 void plan_release(Plan& P);
+int plan_profile_read(Plan& P, int kind, double* ms, int64_t* launches, double* flops, double* bytes);
 
 }  // namespace tq

@@ -1,0 +1,325 @@
+"""Equation parsing, contraction-path finding and index slicing (host side of the engine).
+
+The reference delegates all of this to opt_einsum (tneq_qc/contractor/einsum_strategy.py:622-643,
+`optimize=Configuration.opt_einsum_optimize='greedy'`, tneq_qc/config.py:3; the workload uses
+`optimize="auto"`, symmetry_breaking_quantum.py:142,154,213).  opt_einsum is an unpinned, absent
+third-party dependency, so the build ships its own path finders:
+
+  * ``greedy``  — opt_einsum's greedy rule (pick the connected pair whose contraction removes the
+                  most size: size(out) - size(a) - size(b)), heap-driven, O(E log E);
+  * ``linear``  — a sweep: grow one running tensor by absorbing, among the tensors connected to it,
+                  the one that keeps it smallest (ties broken by an order hint, e.g. (qubit, time)).
+                  For quantum circuits this yields the qubit-by-qubit sweep whose every step is a
+                  small-operand absorption (the APPLY lowering of the plan compiler);
+  * ``partition`` — a tree: sweep each group of a partition, then contract the group results
+                  (e.g. the left/right halves of a circuit cut: the boundary GEMM);
+and a slicer that removes contracted modes (index slicing).
+
+The path only changes summation order (rounding), never the mathematical result; symbol
+bookkeeping (which output axis is which) is preserved exactly.
+"""
+from __future__ import annotations
+
+import heapq
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+
+def get_symbol(i: int) -> str:
+    """opt_einsum.get_symbol semantics (used for core names and einsum symbols throughout the
+    reference: qctn.py:498, einsum_strategy.py:162-182, greedy_strategy.py:414)."""
+    if i < 52:
+        return "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ"[i]
+    if i >= 55296:
+        return chr(i + 2048)
+    return chr(i + 140)
+
+
+@dataclass
+class Network:
+    """An einsum as integer modes: terms[i] = mode ids of operand i, out = output mode ids."""
+    terms: List[List[int]]
+    out: List[int]
+    extents: Dict[int, int]
+    symbols: List[str] = field(default_factory=list)  # mode id -> original symbol
+
+    def size(self, modes: Iterable[int]) -> int:
+        p = 1
+        for m in modes:
+            p *= self.extents[m]
+        return p
+
+
+def parse_equation(eq: str, shapes: Sequence[Sequence[int]]) -> Network:
+    """Parse "ab,bc->ac" (any unicode symbols, explicit or implicit output) into a Network."""
+    eq = eq.replace(" ", "")
+    if "->" in eq:
+        lhs, rhs = eq.split("->")
+        implicit = False
+    else:
+        lhs, rhs, implicit = eq, "", True
+    terms_s = lhs.split(",") if lhs != "" else []
+    if len(terms_s) != len(shapes):
+        raise ValueError(f"einsum equation has {len(terms_s)} operands but {len(shapes)} shapes were given")
+    if implicit:
+        cnt: Dict[str, int] = {}
+        for ch in lhs.replace(",", ""):
+            cnt[ch] = cnt.get(ch, 0) + 1
+        rhs = "".join(sorted(c for c, k in cnt.items() if k == 1))
+    sym2id: Dict[str, int] = {}
+    symbols: List[str] = []
+    extents: Dict[int, int] = {}
+    terms: List[List[int]] = []
+    for t, shp in zip(terms_s, shapes):
+        shp = tuple(int(x) for x in shp)
+        if len(t) != len(shp):
+            raise ValueError(f"term {t!r} has {len(t)} symbols but the operand has shape {shp}")
+        ids = []
+        for ch, e in zip(t, shp):
+            if ch not in sym2id:
+                sym2id[ch] = len(symbols)
+                symbols.append(ch)
+            m = sym2id[ch]
+            if m in ids:
+                raise ValueError(f"repeated symbol {ch!r} inside one operand (diagonals) is not supported")
+            if extents.setdefault(m, e) != e:
+                raise ValueError(f"symbol {ch!r} has inconsistent extents {extents[m]} vs {e}")
+            ids.append(m)
+        terms.append(ids)
+    out = []
+    for ch in rhs:
+        if ch not in sym2id:
+            raise ValueError(f"output symbol {ch!r} does not appear in any operand")
+        if sym2id[ch] in out:
+            raise ValueError(f"output symbol {ch!r} repeated")
+        out.append(sym2id[ch])
+    return Network(terms, out, extents, symbols)
+
+
+# ---------------------------------------------------------------------------------------------
+# path finders — all return an opt_einsum-style SSA path: list of (i, j); new id = n + step
+# ---------------------------------------------------------------------------------------------
+
+class _State:
+    def __init__(self, net: Network):
+        self.net = net
+        self.live: Dict[int, Tuple[int, ...]] = {i: tuple(t) for i, t in enumerate(net.terms)}
+        self.owners: Dict[int, set] = {}
+        for i, t in self.live.items():
+            for m in t:
+                self.owners.setdefault(m, set()).add(i)
+        self.outset = set(net.out)
+        self.next_id = len(net.terms)
+
+    def result(self, i: int, j: int) -> Tuple[int, ...]:
+        ti, tj = self.live[i], self.live[j]
+        res = []
+        seen = set()
+        for m in ti + tj:
+            if m in seen:
+                continue
+            seen.add(m)
+            own = self.owners[m]
+            if m in self.outset or len(own - {i, j}) > 0:
+                res.append(m)
+        return tuple(res)
+
+    def contract(self, i: int, j: int) -> int:
+        res = self.result(i, j)
+        for m in self.live[i] + self.live[j]:
+            self.owners[m].discard(i)
+            self.owners[m].discard(j)
+        del self.live[i], self.live[j]
+        k = self.next_id
+        self.next_id += 1
+        self.live[k] = res
+        for m in res:
+            self.owners.setdefault(m, set()).add(k)
+        return k
+
+    def neighbours(self, i: int) -> set:
+        nb = set()
+        for m in self.live[i]:
+            nb |= self.owners[m]
+        nb.discard(i)
+        return nb
+
+
+def greedy_path(net: Network) -> List[Tuple[int, int]]:
+    """opt_einsum-style greedy: repeatedly contract the connected pair with the smallest
+    size(result) - size(a) - size(b); disconnected leftovers are joined smallest-first."""
+    st = _State(net)
+    size = net.size
+    heap: List[Tuple[int, int, int, int]] = []
+
+    def push(i, j):
+        if i > j:
+            i, j = j, i
+        c = size(st.result(i, j)) - size(st.live[i]) - size(st.live[j])
+        heapq.heappush(heap, (c, i, j, 0))
+
+    for i in list(st.live):
+        for j in st.neighbours(i):
+            if i < j:
+                push(i, j)
+    path = []
+    while len(st.live) > 1:
+        while heap and (heap[0][1] not in st.live or heap[0][2] not in st.live):
+            heapq.heappop(heap)
+        if heap:
+            _, i, j, _ = heapq.heappop(heap)
+        else:  # no connected pair: outer-product the two smallest tensors
+            ids = sorted(st.live, key=lambda t: (size(st.live[t]), t))
+            i, j = ids[0], ids[1]
+        path.append((i, j))
+        k = st.contract(i, j)
+        for nb in st.neighbours(k):
+            push(k, nb)
+    return path
+
+
+def linear_path(net: Network, order: Optional[Sequence[int]] = None,
+                subset: Optional[Sequence[int]] = None) -> Tuple[List[Tuple[int, int]], int]:
+    """Sweep path over `subset` (default: all operands): start from the first tensor of the order
+    hint and repeatedly absorb the connected tensor that keeps the running tensor smallest
+    (ties: earliest in the order hint).  Returns (path over the full SSA numbering, final id).
+    Only tensors of `subset` are touched; the caller continues the numbering."""
+    ids = list(range(len(net.terms))) if subset is None else list(subset)
+    if order is None:
+        order = ids
+    rank = {t: k for k, t in enumerate(order)}
+    for t in ids:
+        rank.setdefault(t, len(rank) + t)
+    st = _State(net)
+    return _linear_on_state(st, ids, rank)
+
+
+def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int]):
+    size = st.net.size
+    remaining = set(ids)
+    first = min(remaining, key=lambda t: rank[t])
+    remaining.discard(first)
+    cur = first
+    path = []
+    while remaining:
+        cand = st.neighbours(cur) & remaining
+        if not cand:
+            nxt = min(remaining, key=lambda t: rank[t])
+        else:
+            nxt = min(cand, key=lambda t: (size(st.result(cur, t)), rank[t]))
+        remaining.discard(nxt)
+        path.append((cur, nxt))
+        cur = st.contract(cur, nxt)
+    return path, cur
+
+
+def partition_path(net: Network, groups: Sequence[Sequence[int]],
+                   orders: Optional[Sequence[Sequence[int]]] = None) -> List[Tuple[int, int]]:
+    """Sweep each group with linear_path, then contract the group results left to right."""
+    st = _State(net)
+    path: List[Tuple[int, int]] = []
+    roots = []
+    for g, grp in enumerate(groups):
+        order = orders[g] if orders is not None else list(grp)
+        rank = {t: k for k, t in enumerate(order)}
+        for t in grp:
+            rank.setdefault(t, len(rank) + t)
+        p, root = _linear_on_state(st, list(grp), rank)
+        path += p
+        roots.append(root)
+    cur = roots[0]
+    for r in roots[1:]:
+        path.append((cur, r))
+        cur = st.contract(cur, r)
+    return path
+
+
+@dataclass
+class PathInfo:
+    flops: float            # complex-MAC count of a full execute (sum over steps of the product
+                            # of all extents involved; sliced steps counted once per slice)
+    max_size: int           # largest intermediate (elements)
+    steps: List[Tuple[int, int, Tuple[int, ...], float]]  # (i, j, result modes, macs per run)
+    once_flops: float = 0.0   # slice-invariant part (hoisted by the plan executor)
+    slice_flops: float = 0.0  # per-slice part
+    n_slices: int = 1
+    est_seconds: float = 0.0  # roofline estimate of a full execute on one MI355X
+
+
+# roofline constants for the cost model (MI355X: ~5 TB/s achievable HBM, ~110 TF/s sustained
+# fp32-MFMA GEMM); only ratios matter for path / slice choices
+_BW, _PEAK, _ESZ, _FPM = 5.0e12, 1.1e14, 8.0, 8.0
+
+
+def path_info(net: Network, path: Sequence[Tuple[int, int]], removed: Iterable[int] = ()) -> PathInfo:
+    """Cost of a path; modes in `removed` (sliced) count with extent 1.  Steps that touch no
+    sliced input are slice-invariant: the native plan hoists them out of the slice loop."""
+    removed = set(removed)
+    ext = {m: (1 if m in removed else e) for m, e in net.extents.items()}
+    st = _State(net)
+    size = lambda ms: math.prod(ext[m] for m in ms)
+    dep = {i: any(m in removed for m in t) for i, t in st.live.items()}
+    n_sl = math.prod(net.extents[m] for m in removed) if removed else 1
+    once = per = t_once = t_per = 0.0
+    mx = max([size(t) for t in st.live.values()] + [1])
+    steps = []
+    for i, j in path:
+        if i not in st.live or j not in st.live:
+            raise ValueError(f"invalid path step ({i}, {j})")
+        union = set(st.live[i]) | set(st.live[j])
+        macs = float(size(union))
+        si, sj = size(st.live[i]), size(st.live[j])
+        k = st.contract(i, j)
+        dep[k] = dep[i] or dep[j]
+        sk = size(st.live[k])
+        t = max((si + sj + sk) * _ESZ / _BW, macs * _FPM / _PEAK) + 2e-6  # + launch
+        if dep[k]:
+            per += macs
+            t_per += t
+        else:
+            once += macs
+            t_once += t
+        mx = max(mx, sk)
+        steps.append((i, j, st.live[k], macs))
+    if len(st.live) != 1:
+        raise ValueError("path does not contract the network to one tensor")
+    return PathInfo(once + per * n_sl, mx, steps, once, per, n_sl, t_once + t_per * n_sl)
+
+
+def validate_path(n_terms: int, path: Sequence[Tuple[int, int]]) -> None:
+    used = set()
+    for s, (i, j) in enumerate(path):
+        nid = n_terms + s
+        for x in (i, j):
+            if not (0 <= x < nid) or x in used:
+                raise ValueError(f"invalid path step {s}: ({i}, {j})")
+            used.add(x)
+        if i == j:
+            raise ValueError(f"invalid path step {s}: ({i}, {j})")
+    if len(path) != max(0, n_terms - 1):
+        raise ValueError(f"a pairwise path needs {n_terms - 1} steps, got {len(path)}")
+
+
+def choose_slices(net: Network, path: Sequence[Tuple[int, int]], n_modes: int,
+                  candidates: Optional[Sequence[int]] = None) -> List[int]:
+    """Greedy index slicing: repeatedly fix the contracted mode whose removal minimises the
+    roofline time of an execute = hoisted slice-invariant steps + slices x per-slice steps.
+    Output modes are never sliced."""
+    outset = set(net.out)
+    if candidates is None:
+        candidates = [m for m in net.extents if m not in outset]
+    chosen: List[int] = []
+    for _ in range(n_modes):
+        best = None
+        for m in candidates:
+            if m in chosen or m in outset:
+                continue
+            info = path_info(net, path, chosen + [m])
+            key = (info.est_seconds, info.max_size, m)
+            if best is None or key < best[0]:
+                best = (key, m)
+        if best is None:
+            break
+        chosen.append(best[1])
+    return chosen

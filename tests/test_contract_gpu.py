@@ -1,0 +1,135 @@
+"""Parity of the HIP contraction path (native plan: APPLY / permute / MFMA GEMM, slicing,
+hoisting) against the oracle's exact numpy pairwise executor on identical inputs.
+
+Tolerances (relative to max |reference|): complex128 1e-12, complex64 2e-5 — the fp64 / fp32
+bounds of north_star ("amplitudes match ... to a stated fp64 tolerance").
+"""
+import numpy as np
+import pytest
+
+from oracle.contract_ref import contract as ref_contract
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"complex128": 1e-12, "complex64": 2e-5, "float64": 1e-12, "float32": 2e-5}
+
+
+def _err(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(1e-300, np.abs(b).max()))
+
+
+def _run(task_or_eq, operands, dtype, dev, **kw):
+    import torch
+    from tneq_qc_amd.expression import HipContractExpression
+    eq, shapes = task_or_eq
+    e = HipContractExpression(eq, *shapes, **kw)
+    ts = [torch.from_numpy(np.ascontiguousarray(o)).to(dev, getattr(torch, dtype)) for o in operands]
+    return e, e(*ts).cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_c1_single_amplitude(dev, dtype):
+    from tneq_qc_amd.circuits import config_task
+    t = config_task("C1")
+    ref = ref_contract(t.eq, *t.operands)
+    _, out = _run((t.eq, t.shapes), t.operands, dtype, dev, optimize=t.path)
+    assert _err(out, ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_full_state_vector_unitarity(dev, dtype):
+    """10q depth-8, all outputs open: psi matches the oracle and sum |psi|^2 == 1 (KAT 1)."""
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task
+    t = amplitude_task(BrickWall(10, 8, 3), list(range(10)))
+    ref = ref_contract(t.eq, *t.operands)
+    for opt in (t.path, "greedy"):
+        _, out = _run((t.eq, t.shapes), t.operands, dtype, dev, optimize=opt)
+        assert out.shape == (2,) * 10
+        assert _err(out, ref) < TOL[dtype]
+        assert abs((np.abs(out) ** 2).sum() - 1.0) < (1e-12 if dtype == "complex128" else 1e-5)
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_cut_sliced_batch(dev, dtype):
+    """Cut tree + index slicing (+ slice-invariant hoisting) == oracle; partial slice ranges sum."""
+    import torch
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task
+    t = amplitude_task(BrickWall(14, 8, 5), list(range(4, 10)), cut=7, n_slice=3)
+    assert len(t.sliced) == 3
+    ref = ref_contract(t.eq, *t.operands)
+    e, out = _run((t.eq, t.shapes), t.operands, dtype, dev, optimize=t.path, slices=t.sliced)
+    assert e.n_slices == 8
+    assert _err(out, ref) < TOL[dtype]
+    # ranks 0..3 of a 4-way shard, accumulated into one buffer == the full sum
+    ts = [torch.from_numpy(np.ascontiguousarray(o)).to(dev, getattr(torch, dtype)) for o in t.operands]
+    acc = torch.zeros(e.out_shape, dtype=getattr(torch, dtype), device=dev)
+    for r in range(4):
+        e(*ts, out=acc, slice_range=(r, 8, 4), accumulate=True)
+    assert _err(acc.cpu().numpy(), ref) < TOL[dtype]
+
+
+def test_core_only_ansatz_split_merge(dev):
+    """C5 shape: the symmetry-breaking ansatz core-only contraction (einsum_strategy.py:136-194),
+    complex128, via greedy and via the split/merge partition (qctn.py:1296-1506)."""
+    from tneq_qc_amd.circuits import ansatz_qctn
+    from tneq_qc_amd.contractor import EinsumStrategy
+    from tneq_qc_amd.einsum import parse_equation, partition_path
+    bw = ansatz_qctn()
+    q = bw.qctn
+    eq, shapes = EinsumStrategy.build_core_only_expression(q)
+    ops = [bw.cores[c] for c in q.cores]
+    ref = ref_contract(eq, *ops)
+    assert ref.shape == (2,) * 16
+    _, out = _run((eq, shapes), ops, "complex128", dev, optimize="greedy")
+    assert _err(out, ref) < 1e-12
+    half = q.ncores // 2
+    path = partition_path(parse_equation(eq, shapes), [list(range(half)), list(range(half, q.ncores))])
+    e, out2 = _run((eq, shapes), ops, "complex128", dev, optimize=path)
+    assert _err(out2, ref) < 1e-12
+    # the unitary circuit's core-only tensor is a 256 x 256 unitary (in legs x out legs)
+    d = q.ncores  # noqa: F841
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float64", "complex64", "complex128"])
+def test_random_networks_with_batch_modes(dev, dtype):
+    """Random einsums incl. hyperedges (batch modes in 3+ operands and the output)."""
+    rng = np.random.default_rng(11)
+    letters = "abcdefghijklmnopq"
+    for trial in range(12):
+        nt = int(rng.integers(2, 6))
+        ext = {c: int(rng.integers(1, 4)) for c in letters[:10]}
+        terms = ["".join(rng.choice(list(letters[:10]), size=int(rng.integers(1, 5)), replace=False))
+                 for _ in range(nt)]
+        allc = sorted(set("".join(terms)))
+        out = "".join(c for c in allc if rng.random() < 0.35)
+        eq = ",".join(terms) + "->" + out
+        ops = []
+        for tm in terms:
+            x = rng.standard_normal([ext[c] for c in tm])
+            if dtype.startswith("complex"):
+                x = x + 1j * rng.standard_normal(x.shape)
+            ops.append(x.astype(dtype))
+        ref = ref_contract(eq, *ops)
+        _, got = _run((eq, [o.shape for o in ops]), ops, dtype, dev, optimize="greedy")
+        assert got.shape == ref.shape, eq
+        assert _err(got, ref) < TOL[dtype] * 10, (eq, trial)
+
+
+def test_autograd_matches_torch(dev):
+    """Gradients of a HIP expression (conj-other-operands rule) vs torch.einsum autograd."""
+    import torch
+    from tneq_qc_amd.expression import HipContractExpression
+    rng = np.random.default_rng(2)
+    a = rng.standard_normal((2, 3, 4)) + 1j * rng.standard_normal((2, 3, 4))
+    b = rng.standard_normal((4, 5)) + 1j * rng.standard_normal((4, 5))
+    c = rng.standard_normal((5, 2)) + 1j * rng.standard_normal((5, 2))
+    eq = "ijk,kl,lm->ijm"
+    e = HipContractExpression(eq, a.shape, b.shape, c.shape)
+    tg = [torch.tensor(x, dtype=torch.complex128, device=dev, requires_grad=True) for x in (a, b, c)]
+    tc = [torch.tensor(x, dtype=torch.complex128, requires_grad=True) for x in (a, b, c)]
+    out = e(*tg)
+    (out.abs() ** 2).sum().backward()
+    ref = torch.einsum(eq, *tc)
+    (ref.abs() ** 2).sum().backward()
+    for g, r in zip(tg, tc):
+        assert _err(g.grad.cpu().numpy(), r.grad.numpy()) < 1e-12
