@@ -120,10 +120,11 @@ def main():
     out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
     t_plan = time.perf_counter() - t_plan0
 
+    from tneq_qc_amd.distributed import SlicedContraction
+    job = SlicedContraction(expr)   # slices rank, rank+N, ... + one RCCL all-reduce (SUM)
+
     def step():
-        expr(*ops, out=out, slice_range=(rank, n_slices, world))
-        if world > 1:
-            dist.all_reduce(torch.view_as_real(out), op=dist.ReduceOp.SUM)
+        job(*ops, out=out)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,109 @@
+"""Host planner + native plan compiler on the CPU (no GPU needed: tq_plan_create only compiles;
+device memory is taken at the first execute).  Also checks the C ABI exports."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import tneq_qc_amd
+from tneq_qc_amd import _lib
+from tneq_qc_amd.circuits import BrickWall, amplitude_task, config_task
+from tneq_qc_amd.einsum import (choose_slices, greedy_path, linear_path, parse_equation,
+                                partition_path, path_info, validate_path)
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_library_exports_every_header_symbol():
+    header = (ROOT / "include" / "tneqhip.h").read_text()
+    declared = set(re.findall(r"\b(tq_[a-z_]+)\s*\(", header))
+    L = _lib.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert declared == set(_lib.EXPORTED)
+    assert L.tq_version() >= 1
+
+
+def test_parse_equation_errors():
+    with pytest.raises(ValueError):
+        parse_equation("ab,bc->ac", [(2, 3)])
+    with pytest.raises(ValueError):
+        parse_equation("ab,bc->ac", [(2, 3), (4, 2)])
+    with pytest.raises(ValueError):
+        parse_equation("aa->a", [(2, 2)])
+    with pytest.raises(ValueError):
+        parse_equation("ab->c", [(2, 2)])
+    n = parse_equation("ab,bc", [(2, 3), (3, 4)])   # implicit output = 'ac'
+    assert [n.symbols[m] for m in n.out] == ["a", "c"]
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_paths_valid_and_sweep_is_narrow(cfg):
+    t = config_task(cfg)
+    net = t.network()
+    validate_path(len(net.terms), t.path)
+    info = path_info(net, t.path)
+    d = t.circuit.depth
+    assert info.max_size <= 2 ** (d + 2)          # a line sweep keeps ~2^d legs
+    g = greedy_path(net)
+    validate_path(len(net.terms), g)
+    lp, root = linear_path(net)
+    validate_path(len(net.terms), lp)
+
+
+def test_partition_and_slicing_choose_cut_legs():
+    t = amplitude_task(BrickWall(14, 8, 1), list(range(4, 10)), cut=7, n_slice=2)
+    net = t.network()
+    sl = [net.symbols.index(s) for s in t.sliced]
+    assert not set(sl) & set(net.out)
+    info0 = path_info(net, t.path)
+    info = path_info(net, t.path, sl)
+    assert info.n_slices == 4
+    assert info.slice_flops < info0.flops
+
+
+def _plan(task, dtype="complex64"):
+    import torch
+    from tneq_qc_amd.expression import HipContractExpression
+    e = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
+    return e, e.plan(getattr(torch, dtype))
+
+
+def test_native_plan_lowering_c1_is_all_apply():
+    e, p = _plan(config_task("C1"))
+    assert p.query("n_apply") == p.query("n_kernels")   # every sweep step = one APPLY pass
+    assert p.query("n_permute") == 0 and p.query("n_gemm") == 0
+    assert p.n_slices == 1
+
+
+def test_native_plan_c4_structure():
+    e, p = _plan(config_task("C4"))
+    assert p.n_slices == 8
+    assert p.query("n_gemm") == 1                        # the boundary GEMM
+    d = p.describe().splitlines()
+    gemm = [l for l in d if "GEMM" in l]
+    assert "M=1024 N=1024" in gemm[0] and "[slice]" in gemm[0]
+    assert p.query("n_ops_once") > 0.5 * p.query("n_kernels")   # most of the sweep is hoisted
+    assert p.query("flops") == pytest.approx(p.query("flops_once") + 8 * p.query("flops_slice"), rel=1e-6)
+
+
+def test_plan_rejects_bad_paths():
+    from tneq_qc_amd.expression import HipContractExpression
+    with pytest.raises(ValueError):
+        HipContractExpression("ab,bc,cd->ad", (2, 2), (2, 2), (2, 2), optimize=[(0, 1), (0, 2)])
+    with pytest.raises(ValueError):
+        HipContractExpression("ab,bc->ac", (2, 2), (2, 2), slices=["a"])
+
+
+def test_plan_create_errors_map_to_valueerror():
+    import torch
+    from tneq_qc_amd.expression import NativePlan
+    from tneq_qc_amd.einsum import Network
+    net = Network([[0, 1], [1, 2]], [0, 2], {0: 2, 1: 3, 2: 2})
+    with pytest.raises(ValueError):
+        NativePlan(net, [(0, 0)], torch.complex64, None, [])
+    net_bad = Network([[0, 1], [1, 2]], [0, 2], {0: 2, 1: 3, 2: 2})
+    with pytest.raises(ValueError):          # a sliced mode that is an output mode
+        NativePlan(net_bad, [(0, 1)], torch.complex64, None, [0])

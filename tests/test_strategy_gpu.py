@@ -1,0 +1,137 @@
+"""The plugin surface on the GPU: BackendHIP via BackendFactory, the 'balanced' HipTreeStrategy
+(L·M·R sandwich) vs the oracle's literal GreedyStrategy restatement, EngineSiamese probabilities,
+TNTensor scale semantics, and the symmetry-breaking core-only workload through the backend."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def backend(dev):
+    from tneq_qc_amd.backends import BackendFactory
+    return BackendFactory.create_backend("hip", device="cuda:0", dtype="complex128")
+
+
+def _setup(n=4, cells=2, seed=5):
+    from oracle.qctn_ref import QCTNRef, random_cores
+    from tneq_qc_amd.circuits import build_brick_wall_IM, incidence_to_graph
+    g = incidence_to_graph(build_brick_wall_IM(n, cells))
+    return g, QCTNRef(g), random_cores(QCTNRef(g), seed)
+
+
+def test_factory_and_errors(dev):
+    from tneq_qc_amd.backends import BackendFactory, BackendHIP
+    b = BackendFactory.create_backend("hip", dtype="complex64")
+    assert isinstance(b, BackendHIP) and b.get_backend_name() == "hip"
+    with pytest.raises(ValueError):
+        BackendFactory.create_backend("nope")
+    with pytest.raises(ValueError):
+        BackendFactory.create_backend("hip", dtype="int8")
+
+
+@pytest.mark.parametrize("mx_kind", ["projector", "random3", "random4"])
+def test_balanced_strategy_matches_oracle_greedy(backend, mx_kind):
+    import torch
+    from oracle.greedy_ref import greedy_contract
+    from tneq_qc_amd.contractor import StrategyCompiler
+    from tneq_qc_amd.core import QCTN
+    g, qr, cores = _setup()
+    q = QCTN(g)
+    n = q.nqubits
+    rng = np.random.default_rng(1)
+    states = [np.array([1.0, 0.0], complex) for _ in range(n)]
+    B = 3
+    if mx_kind == "projector":
+        mx = [np.stack([np.diag(np.eye(2)[rng.integers(2)]) for _ in range(B)]).astype(complex) for _ in range(n)]
+    elif mx_kind == "random3":
+        mx = [rng.standard_normal((B, 2, 2)) + 1j * rng.standard_normal((B, 2, 2)) for _ in range(n)]
+    else:
+        mx = [rng.standard_normal((B, 2, 2, 2)) + 1j * rng.standard_normal((B, 2, 2, 2)) for _ in range(n)]
+    ref = greedy_contract(qr, cores, states, mx)
+    fn, name, cost = StrategyCompiler("balanced").compile(
+        q, {"circuit_states_shapes": tuple(s.shape for s in states),
+            "measure_shapes": tuple(m.shape for m in mx), "measure_is_matrix": True}, backend)
+    assert name == "hip_tree"
+    T = lambda x: torch.from_numpy(x).to("cuda:0")
+    got = fn({c: T(cores[c]) for c in q.cores}, [T(s) for s in states], [T(m) for m in mx]).cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-12
+
+
+def test_engine_probabilities_and_tntensor(backend):
+    """EngineSiamese: full = Born rule (|.|^2 of the sandwich), conditional = joint/marginal
+    (tests/test_probabilities.py:84-88 assertion), TNTensor scales multiply."""
+    import torch
+    from oracle.greedy_ref import greedy_contract
+    from tneq_qc_amd.core import QCTN, TNTensor
+    from tneq_qc_amd.core.engine_siamese import EngineSiamese
+    g, qr, cores = _setup(3, 2, 7)
+    q = QCTN(g)
+    T = lambda x: torch.from_numpy(np.asarray(x)).to("cuda:0")
+    q.cores_weights = {c: T(cores[c]) for c in q.cores}
+    eng = EngineSiamese(backend, "balanced")
+    states = [T(np.array([1.0, 0.0], complex)) for _ in range(3)]
+    P0 = np.array([[1, 0], [0, 0]], complex)[None].repeat(4, 0)
+    full = eng.calculate_full_probability(q, states, [T(P0)] * 3).cpu().numpy()
+    sand = greedy_contract(qr, cores, [np.array([1.0, 0.0], complex)] * 3, [P0] * 3)
+    assert np.allclose(full, np.abs(sand) ** 2, atol=1e-14)
+    joint = eng.calculate_marginal_probability(q, states, [T(P0), T(P0)], [0, 1]).cpu().numpy()
+    marg = eng.calculate_marginal_probability(q, states, [T(P0)], [1]).cpu().numpy()
+    cond = eng.calculate_conditional_probability(q, states, [T(P0), T(P0)], [0, 1], [0]).cpu().numpy()
+    assert np.allclose(cond, joint / (marg + 1e-10), atol=1e-10)
+    # TNTensor cores: result scale = product of every core's scale twice (L and R)
+    q2 = QCTN(g)
+    q2.cores_weights = {c: TNTensor(T(cores[c]) / 2.0, 2.0) for c in q.cores}
+    eng2 = EngineSiamese(backend, "balanced")
+    full2 = eng2.calculate_full_probability(q2, states, [T(P0)] * 3).cpu().numpy()
+    assert np.allclose(full2, full, atol=1e-13)
+
+
+def test_backend_einsum_permute_and_core_only_workload(backend):
+    """The symmetry-breaking hot loop shape (symmetry_breaking_quantum.py:210-228): core-only
+    expression of the masked 8-qubit ansatz, fidelity with a target, on the HIP backend."""
+    import torch
+    from oracle.contract_ref import contract as ref_contract
+    from tneq_qc_amd.circuits import ansatz_qctn
+    from tneq_qc_amd.contractor import EinsumStrategy
+    bw = ansatz_qctn()
+    q = bw.qctn
+    eq, shapes = EinsumStrategy.build_core_only_expression(q)
+    expr = EinsumStrategy.create_contract_expression(eq, shapes, optimize="auto")
+    params = [backend.convert_to_tensor(bw.cores[c]) for c in q.cores]
+    out = backend.execute_expression(expr, *params)
+    ref = ref_contract(eq, *[bw.cores[c] for c in q.cores])
+    assert np.abs(out.cpu().numpy() - ref).max() < 1e-12
+    tar = out.reshape(-1)
+    fid = (torch.vdot(tar, out.reshape(-1)).abs() ** 2 / (torch.vdot(tar, tar).real ** 2)).item()
+    assert abs(fid - 1) < 1e-12
+    x = backend.convert_to_tensor(np.arange(24.0).reshape(2, 3, 4))
+    assert torch.equal(backend.permute(x, (2, 0, 1)), x.permute(2, 0, 1).contiguous())
+    e = backend.einsum("ijk,kl->lij", x, backend.convert_to_tensor(np.ones((4, 5))))
+    assert torch.allclose(e, torch.einsum("ijk,kl->lij", x, torch.ones(4, 5, dtype=x.dtype, device=x.device)))
+
+
+def test_training_step_gradients_through_hip(backend):
+    """Fidelity loss + backward through the HIP expression (the C5 training loop shape)."""
+    import torch
+    from tneq_qc_amd.circuits import BrickWall
+    from tneq_qc_amd.contractor import EinsumStrategy
+    bw = BrickWall(4, 4, 1)
+    q = bw.qctn
+    eq, shapes = EinsumStrategy.build_core_only_expression(q)
+    expr = EinsumStrategy.create_contract_expression(eq, shapes)
+    tgt = expr(*[backend.convert_to_tensor(bw.cores[c]) for c in q.cores]).detach().reshape(-1)
+    params = [torch.nn.Parameter(backend.convert_to_tensor(bw.cores[c] * 1.01)) for c in q.cores]
+    out = expr(*params).reshape(-1)
+    loss = 1.0 - torch.vdot(tgt, out).abs() ** 2 / (torch.vdot(tgt, tgt).real * torch.vdot(out, out).real)
+    loss.backward()
+    # same loss with torch.einsum on CPU as the gradient reference
+    cp = [torch.tensor(bw.cores[c] * 1.01, requires_grad=True) for c in q.cores]
+    o2 = torch.einsum(eq, *cp).reshape(-1) if len(set(eq)) <= 60 else None
+    if o2 is not None:
+        t2 = tgt.cpu()
+        l2 = 1.0 - torch.vdot(t2, o2).abs() ** 2 / (torch.vdot(t2, t2).real * torch.vdot(o2, o2).real)
+        l2.backward()
+        for p, r in zip(params, cp):
+            assert torch.allclose(p.grad.cpu(), r.grad, atol=1e-10)
