@@ -21,7 +21,8 @@ import numpy as np
 
 from .contractor.einsum_strategy import EinsumStrategy
 from .core.qctn import QCTN
-from .einsum import Network, choose_slices, get_symbol, parse_equation, partition_path, linear_path
+from .einsum import (Network, choose_slices, get_symbol, linear_path, parse_equation, partition_path,
+                     vector_absorptions)
 
 
 def build_brick_wall_IM(n_qubits: int, n_cells: int, rank: int = 2) -> np.ndarray:
@@ -162,7 +163,8 @@ class AmplitudeTask:
 
 
 def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Optional[Dict[int, int]] = None,
-                   cut: Optional[int] = None, n_slice: int = 0, bit_seed: int = 7) -> AmplitudeTask:
+                   cut: Optional[int] = None, n_slice: int = 0, bit_seed: int = 7,
+                   absorb_vectors: bool = True) -> AmplitudeTask:
     """Build the amplitude network; fixed bits default to a seeded uniform bitstring."""
     n = circ.n_qubits
     open_set = set(int(q) for q in open_qubits)
@@ -198,9 +200,12 @@ def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Opti
             line, t = v, (-1 if kind == "in" else 10 ** 6)
         return (line if upward else -line, t)
 
+    # inputs |0> and output projectors are folded into their gates first (no sweep step then
+    # grows the running tensor by a leg that a vector removes right after)
+    pre = vector_absorptions(net) if absorb_vectors else []
     if cut is None:
         order = sorted(range(len(kinds)), key=lambda i: sweep_key(kinds[i]))
-        path = linear_path(net, order)[0]
+        path = linear_path(net, order, pre=pre)[0]
         sliced_ids: List[int] = []
     else:
         # cores go left when their lower qubit is < cut (the gates straddling the cut are
@@ -219,7 +224,7 @@ def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Opti
         right = [i for i in range(len(kinds)) if not side[i]]
         lord = sorted(left, key=lambda i: sweep_key(kinds[i], True))
         rord = sorted(right, key=lambda i: sweep_key(kinds[i], False))
-        path = partition_path(net, [left, right], [lord, rord])
+        path = partition_path(net, [left, right], [lord, rord], pre=pre)
         lm = set(m for i in left for m in net.terms[i])
         rm = set(m for i in right for m in net.terms[i])
         cut_modes = sorted((lm & rm) - set(net.out))

@@ -179,11 +179,66 @@ def greedy_path(net: Network) -> List[Tuple[int, int]]:
     return path
 
 
+def vector_absorptions(net: Network) -> List[Tuple[int, int]]:
+    """Pre-contraction pairs (vector, neighbour) for every rank-1 operand whose single contracted
+    mode is shared with exactly one other operand: product-state inputs and output projectors are
+    folded into their gate before any sweep, so no sweep step ever grows the running tensor by a
+    leg that a vector removes one step later.  A neighbour keeps at least one leg (never becomes
+    a scalar); several vectors on one gate are absorbed one after the other."""
+    owners: Dict[int, List[int]] = {}
+    for i, t in enumerate(net.terms):
+        for m in t:
+            owners.setdefault(m, []).append(i)
+    outset = set(net.out)
+    legs = {i: len(t) for i, t in enumerate(net.terms)}
+    pre = []
+    for i, t in enumerate(net.terms):
+        if len(t) != 1 or t[0] in outset:
+            continue
+        own = [j for j in owners[t[0]] if j != i]
+        if len(own) != 1 or len(net.terms[own[0]]) < 2 or legs[own[0]] <= 1:
+            continue
+        legs[own[0]] -= 1
+        pre.append((i, own[0]))
+    return pre
+
+
+def _apply_pre(st: "_State", pre: Sequence[Tuple[int, int]]):
+    """Contract the (original-id) pairs of `pre` on `st`; returns (path, alias original->live id)."""
+    alias: Dict[int, int] = {}
+    find = lambda x: alias.get(x, x) if alias.get(x, x) == x else find(alias[x])
+    path = []
+    for a, b in pre:
+        ia, ib = find(a), find(b)
+        path.append((ia, ib))
+        k = st.contract(ia, ib)
+        alias[ia] = k
+        alias[ib] = k
+        alias[k] = k
+    return path, find
+
+
+def _alias_group(ids: Sequence[int], find, rank_of: Dict[int, int]):
+    """Map original ids (and an order rank) onto the live ids after pre-contraction."""
+    out: List[int] = []
+    rank: Dict[int, int] = {}
+    for t in ids:
+        k = find(t)
+        if k not in rank:
+            out.append(k)
+            rank[k] = rank_of.get(t, len(rank_of) + t)
+        else:
+            rank[k] = min(rank[k], rank_of.get(t, len(rank_of) + t))
+    return out, rank
+
+
 def linear_path(net: Network, order: Optional[Sequence[int]] = None,
-                subset: Optional[Sequence[int]] = None) -> Tuple[List[Tuple[int, int]], int]:
+                subset: Optional[Sequence[int]] = None,
+                pre: Sequence[Tuple[int, int]] = ()) -> Tuple[List[Tuple[int, int]], int]:
     """Sweep path over `subset` (default: all operands): start from the first tensor of the order
     hint and repeatedly absorb the connected tensor that keeps the running tensor smallest
-    (ties: earliest in the order hint).  Returns (path over the full SSA numbering, final id).
+    (ties: earliest in the order hint).  `pre` = original-id pairs contracted first (e.g.
+    vector_absorptions).  Returns (path over the full SSA numbering, final id).
     Only tensors of `subset` are touched; the caller continues the numbering."""
     ids = list(range(len(net.terms))) if subset is None else list(subset)
     if order is None:
@@ -192,7 +247,10 @@ def linear_path(net: Network, order: Optional[Sequence[int]] = None,
     for t in ids:
         rank.setdefault(t, len(rank) + t)
     st = _State(net)
-    return _linear_on_state(st, ids, rank)
+    path, find = _apply_pre(st, pre)
+    ids, rank = _alias_group(ids, find, rank)
+    p, root = _linear_on_state(st, ids, rank)
+    return path + p, root
 
 
 def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int]):
@@ -215,17 +273,18 @@ def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int]):
 
 
 def partition_path(net: Network, groups: Sequence[Sequence[int]],
-                   orders: Optional[Sequence[Sequence[int]]] = None) -> List[Tuple[int, int]]:
-    """Sweep each group with linear_path, then contract the group results left to right."""
+                   orders: Optional[Sequence[Sequence[int]]] = None,
+                   pre: Sequence[Tuple[int, int]] = ()) -> List[Tuple[int, int]]:
+    """Sweep each group with linear_path, then contract the group results left to right.
+    `pre` pairs (original ids, both in one group) are contracted before the sweeps."""
     st = _State(net)
-    path: List[Tuple[int, int]] = []
+    path, find = _apply_pre(st, pre)
     roots = []
     for g, grp in enumerate(groups):
         order = orders[g] if orders is not None else list(grp)
-        rank = {t: k for k, t in enumerate(order)}
-        for t in grp:
-            rank.setdefault(t, len(rank) + t)
-        p, root = _linear_on_state(st, list(grp), rank)
+        rank0 = {t: k for k, t in enumerate(order)}
+        ids, rank = _alias_group(list(grp), find, rank0)
+        p, root = _linear_on_state(st, ids, rank)
         path += p
         roots.append(root)
     cur = roots[0]
