@@ -15,6 +15,7 @@
 //    output tile count alone cannot fill 256 CUs.
 //  * XCD-aware tile order: tiles that share an A row panel are dealt to the same XCD.
 #include <algorithm>
+#include <cstdlib>
 
 #include "tq_common.h"
 
@@ -59,6 +60,15 @@ struct GemmArgs {
 };
 
 constexpr int kThreads = 256;
+
+// TQ_GEMM_FAST=0 disables the K-outer complex64 fast path (A/B timing of the two kernels)
+bool fast_disabled() {
+  static const int v = [] {
+    const char* e = getenv("TQ_GEMM_FAST");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  return v != 0;
+}
 
 template <typename R>
 __device__ __forceinline__ void mfma(R a, R b, typename std::conditional<sizeof(R) == 4, f32x16, f64x4>::type& c);
@@ -287,6 +297,196 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
       }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Fast path: complex64 with both operands K-outer (A stored K x M, B stored K x N, M / N
+// contiguous) — the layout the plan compiler gives the boundary GEMM of a sliced cut (the
+// dominant contraction of the sliced amplitude workloads).
+//
+//  * 512 threads = 8 waves (2 per SIMD), block tile 256 (M) x 128 (N), wave tile 64 x 64 =
+//    2 x 2 v_mfma_f32_32x32x2_f32 tiles x (re, im) accumulators = 128 AGPRs.
+//  * operands reach LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging): one
+//    wave-instruction moves 1 KiB = 128 complex of one k-row, so the LDS image is the global
+//    row image [k][m] / [k][n] with (re, im) interleaved; a fragment is one ds_read_b64 that
+//    yields (re, im) of one element — lanes 0-31 read 256 contiguous bytes of row k, lanes 32-63
+//    of row k+1: conflict-free.
+//  * 3-stage LDS ring (3 x 48 KiB), two K-tiles in flight: per K-tile one counted
+//    `s_waitcnt vmcnt(6)` (6 DMAs per wave per tile) and ONE raw s_barrier, never vmcnt(0) in the
+//    steady state (cdna_hip_programming.md §5 "Pipelining across barriers").
+//  * split-K over the grid (slab reduce kernel below); a bijective XCD remap puts all tiles of one
+//    K-split on one XCD so each XCD's L2 streams its K range of A and B from HBM exactly once.
+namespace fastc64 {
+constexpr int BM = 256, BN = 128, BK = 16, NT = 512, NSTAGE = 3;
+constexpr int A_FLOATS = BK * BM * 2, B_FLOATS = BK * BN * 2, STAGE = A_FLOATS + B_FLOATS;
+constexpr int A_PIECES_PER_WAVE = (BK * BM * 8 / 1024) / 8;  // 4
+constexpr int B_PIECES_PER_WAVE = (BK * BN * 8 / 1024) / 8;  // 2
+static_assert(A_PIECES_PER_WAVE + B_PIECES_PER_WAVE == 6, "vmcnt count below assumes 6 DMAs/tile");
+}
+
+struct FastArgs {
+  const float* A;  // K x M complex (lda complex elements between k-rows)
+  const float* B;  // K x N complex
+  float* C;        // output (ldc) or split-K slabs
+  float* W;
+  int64_t lda, ldb, ldc, sA, sB, sC, M, N;
+  int64_t kchunk;  // K per split (multiple of BK)
+  int mt, nt, splits, batch;
+  float beta;
+};
+
+__global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArgs g) {
+  using namespace fastc64;
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid & 3, wn = wid >> 2;
+
+  // bijective XCD remap of the linear block id, then (batch, split, tile) with tile fastest
+  const int nblk = gridDim.x;
+  int L = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, xcd = L % 8, idx = L / 8;
+    if (nblk >= 8) L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int ntile = g.mt * g.nt;
+  const int tile = L % ntile;
+  const int split = (L / ntile) % g.splits;
+  const int b = L / (ntile * g.splits);
+  const int tm = tile / g.nt, tn = tile % g.nt;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * g.kchunk;
+  const int nkt = (int)(g.kchunk / BK);
+
+  const float* A = g.A + ((int64_t)b * g.sA + kbeg * g.lda + m0) * 2;
+  const float* B = g.B + ((int64_t)b * g.sB + kbeg * g.ldb + n0) * 2;
+
+  // this wave's DMA pieces: A piece p (0..31) = k-row p/2, m-half p%2; B piece p (0..15) = k-row p.
+  // The DMA is issued from inline asm: hipcc would otherwise treat every in-flight LDS-DMA as a
+  // possible alias of the next ds_read and drain it with vmcnt(0) (cdna_hip_programming.md §5
+  // trap 4(a)); the counted waits below are the only ordering, placed by hand.
+  const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)lds;
+  auto glds16 = [&](const float* gsrc, unsigned lds_off_floats) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + lds_off_floats * 4u);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto issue = [&](int t, int stage) {
+    const unsigned sbase = stage * STAGE;
+#pragma unroll
+    for (int q = 0; q < A_PIECES_PER_WAVE; ++q) {
+      const int p = wid * A_PIECES_PER_WAVE + q;
+      glds16(A + (((int64_t)t * BK + (p >> 1)) * g.lda + (p & 1) * 128 + lane * 2) * 2, sbase + p * 256);
+    }
+#pragma unroll
+    for (int q = 0; q < B_PIECES_PER_WAVE; ++q) {
+      const int p = wid * B_PIECES_PER_WAVE + q;
+      glds16(B + (((int64_t)t * BK + p) * g.ldb + lane * 2) * 2, sbase + A_FLOATS + p * 256);
+    }
+  };
+
+  f32x16 acc_re[2][2], acc_im[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc_re[i][j][r] = 0.f; acc_im[i][j][r] = 0.f; }
+
+  const int fr = lane & 31, fk = lane >> 5;
+  // float offsets of this lane's fragments inside a stage (k-row kk + fk)
+  const int a_off = (fk * BM + wm * 64 + fr) * 2;
+  const int b_off = A_FLOATS + (fk * BN + wn * 64 + fr) * 2;
+
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+  for (int t = 0; t < nkt; ++t) {
+    if (t + 1 < nkt) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (t + 2 < nkt) issue(t + 2, (t + 2) % NSTAGE);
+    const float* s = lds + (t % NSTAGE) * STAGE;
+    // fragments of k-step kk+2 are read while the 16 MFMAs of k-step kk run
+    float2 a[2], bb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const float2*>(s + a_off + (i * 32) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bb[j] = *reinterpret_cast<const float2*>(s + b_off + (j * 32) * 2);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float2 na[2], nb[2];
+      if (kk + 2 < BK) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          na[i] = *reinterpret_cast<const float2*>(s + a_off + ((kk + 2) * BM + i * 32) * 2);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          nb[j] = *reinterpret_cast<const float2*>(s + b_off + ((kk + 2) * BN + j * 32) * 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the k+2 reads ahead of this k-step's MFMAs
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc_re[i][j], 0, 0, 0);
+          acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].y, acc_im[i][j], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(-a[i].y, bb[j].y, acc_re[i][j], 0, 0, 0);
+          acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].x, acc_im[i][j], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kk + 2 < BK) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { a[i] = na[i]; bb[i] = nb[i]; }
+      }
+    }
+  }
+
+  // epilogue: 32x32 f32 MFMA accumulator r of lane -> row (r&3) + 8(r>>2) + 4(lane>>5), col lane&31
+  const bool partial = g.splits > 1;
+  float* Cout = partial ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * 2 : g.C + (int64_t)b * g.sC * 2;
+  const int64_t ldo = partial ? g.N : g.ldc;
+  const float beta = partial ? 0.f : g.beta;
+  auto store = [&](auto with_beta) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int64_t gn = n0 + wn * 64 + j * 32 + (lane & 31);
+          float2* p = reinterpret_cast<float2*>(Cout + (gm * ldo + gn) * 2);
+          float2 v = make_float2(acc_re[i][j][r], acc_im[i][j][r]);
+          if constexpr (decltype(with_beta)::value) {
+            const float2 o = *p;
+            v.x += beta * o.x;
+            v.y += beta * o.y;
+          }
+          *p = v;
+        }
+  };
+  if (beta != 0.f) store(std::true_type{});
+  else store(std::false_type{});
+}
+
+// eligibility and split choice of the fast path (shared by launch and workspace sizing)
+int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  using namespace fastc64;
+  if (!(transA == 1 && transB == 0)) return 0;
+  if (M % BM || N % BN || K % BK || K == 0) return 0;
+  const int64_t tiles = (M / BM) * (N / BN) * batch;
+  int s = 1;
+  // fill the 256 CUs with one block each; keep >= 32 K-tiles per split
+  while (tiles * s * 2 <= 256 && K % ((int64_t)s * 2 * BK) == 0 && K / ((int64_t)s * 2 * BK) >= 32) s *= 2;
+  if (tiles * s > INT32_MAX) return 0;
+  return s;
+}
+
 // C_b = sum_s W[s][b] + beta * C_b
 template <typename R>
 __global__ void __launch_bounds__(kThreads)
@@ -323,6 +523,30 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
   using C_ = Cfg<R>;
   constexpr int EW = CPLX ? 2 : 1;
   constexpr int VE = 16 / (EW * (int)sizeof(R));
+  if constexpr (CPLX && sizeof(R) == 4) {
+    const int fs = fast_c64_splits(transA, transB, M, N, K, batch);
+    const bool al = ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && lda % 2 == 0 &&
+                    ldb % 2 == 0 && (batch == 1 || (sA % 2 == 0 && sB % 2 == 0));
+    const size_t need = (size_t)fs * batch * M * N * 8;
+    if (fs > 0 && al && (fs == 1 || (W != nullptr && wsb >= need)) && !fast_disabled()) {
+      FastArgs f{};
+      f.A = (const float*)A; f.B = (const float*)B; f.C = (float*)C; f.W = (float*)W;
+      f.lda = lda; f.ldb = ldb; f.ldc = ldc; f.sA = sA; f.sB = sB; f.sC = sC; f.M = M; f.N = N;
+      f.kchunk = K / fs; f.mt = (int)(M / fastc64::BM); f.nt = (int)(N / fastc64::BN);
+      f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;
+      const int64_t nblk = (int64_t)f.mt * f.nt * fs * batch;
+      hipLaunchKernelGGL(gemm_c64_kouter_kernel, dim3((unsigned)nblk), dim3(fastc64::NT), 0, stream, f);
+      TQ_HIP(hipGetLastError());
+      if (fs > 1) {
+        const int64_t total = batch * M * N * 2;
+        const int blocks = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 4096);
+        hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(kThreads), 0, stream,
+                           (const float*)W, (float*)C, M, N, ldc, sC, batch, fs, 2, (float)beta);
+        TQ_HIP(hipGetLastError());
+      }
+      return TQ_OK;
+    }
+  }
   GemmArgs g{};
   g.A = A; g.B = B; g.C = C; g.W = W;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
@@ -370,7 +594,8 @@ size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch)
   if (dtype == TQ_F32 || dtype == TQ_C64) { bm = Cfg<float>::BM; bk = Cfg<float>::BK; }
   else { bm = Cfg<double>::BM; bk = Cfg<double>::BK; }
   const int64_t tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm) * batch;
-  const int s = choose_splits(tiles, K, (int)bk);
+  int s = choose_splits(tiles, K, (int)bk);
+  if (dtype == TQ_C64) s = std::max(s, fast_c64_splits(1, 0, M, N, K, batch));
   if (s <= 1) return 0;
   return (size_t)s * batch * M * N * dtype_size(dtype);
 }

@@ -130,3 +130,21 @@ def test_contract_pair_gate_apply(T, dev):
     ref = np.moveaxis(np.tensordot(s.astype("complex128"), g.astype("complex128"), axes=([7, 8], [0, 1])),
                       [18, 19], [7, 8])
     assert np.abs(c - ref).max() / np.abs(ref).max() < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,B,beta", [(256, 128, 16, 1, 0.0), (256, 128, 48, 3, 0.0),
+                                           (512, 256, 4096, 1, 1.0), (1024, 1024, 8192, 1, 0.0),
+                                           (256, 256, 2048, 2, 0.5), (768, 384, 1024, 1, 0.0)])
+def test_gemm_c64_kouter_fast_path(T, dev, M, N, K, B, beta):
+    """complex64 with A stored K x M and B stored K x N: the LDS-DMA fast kernel (3-stage ring,
+    split-K slabs) — shapes on its tile grid, batched, with beta, single and multiple splits."""
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(7)
+    a = _rand(rng, (B, K, M), "complex64")
+    b = _rand(rng, (B, K, N), "complex64")
+    c0 = _rand(rng, (B, M, N), "complex64")
+    cd = _to(T, dev, c0)
+    ops.gemm(_to(T, dev, a), _to(T, dev, b), True, False, out=cd, beta=beta)
+    ref = np.matmul(np.swapaxes(a.astype("complex128"), 1, 2), b.astype("complex128")) + beta * c0
+    err = np.abs(cd.cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err < TOL["complex64"] * np.sqrt(K) * 10, (M, N, K, B, err)
