@@ -162,6 +162,8 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "bytes_slice") return (int64_t)P.bytes_slice;
   if (k == "n_ops_once") { int64_t c = 0; for (auto& o : P.ops) c += o.invariant; return c; }
   if (k == "n_kernels") return (int64_t)P.ops.size();
+  if (k == "graph_builds") return P.graph_builds;
+  if (k == "graph_launches") return P.graph_launches;
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;
   if (k == "n_permute") return P.n_permute;

@@ -20,6 +20,7 @@
 #include "tq_plan.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -644,7 +645,30 @@ int plan_profile_read(Plan& P, int kind, double* ms, int64_t* launches, double* 
   return TQ_OK;
 }
 
+namespace {
+
+bool graphs_disabled() {
+  static const int v = [] {
+    const char* e = getenv("TQ_GRAPH");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
+void drop_graph(Plan& P) {
+  if (P.graph_exec) (void)hipGraphExecDestroy(P.graph_exec);
+  if (P.graph) (void)hipGraphDestroy(P.graph);
+  P.graph_exec = nullptr;
+  P.graph = nullptr;
+  P.has_graph = false;
+}
+
+}  // namespace
+
 void plan_release(Plan& P) {
+  drop_graph(P);
+  if (P.cap_stream) (void)hipStreamDestroy(P.cap_stream);
+  P.cap_stream = nullptr;
   for (auto& ev : P.ev_used) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   for (auto& ev : P.ev_free) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   P.ev_used.clear();
@@ -656,11 +680,45 @@ void plan_release(Plan& P) {
   P.d_arena = P.d_tables = nullptr;
 }
 
+
+int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
+                 int64_t s_step, int accumulate, hipStream_t stream);
+
 int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
              int64_t s_step, int accumulate, hipStream_t stream) {
   TQ_CHECK_ARG(s_step >= 1, "slice_step");
   TQ_CHECK_ARG(s_begin >= 0 && s_end <= P.n_slices, "slice range");
   TQ_CHECK_ARG(P.arena_bytes == 0 || P.d_arena, "plan not materialized");
+  if (P.profile || !P.use_graph || graphs_disabled())
+    return plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, stream);
+  Plan::GraphKey key;
+  key.inputs.assign(inputs, inputs + P.n_inputs);
+  key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
+  if (!(P.has_graph && key == P.gkey)) {
+    drop_graph(P);
+    if (!P.cap_stream) TQ_HIP(hipStreamCreateWithFlags(&P.cap_stream, hipStreamNonBlocking));
+    TQ_HIP(hipStreamBeginCapture(P.cap_stream, hipStreamCaptureModeThreadLocal));
+    const int rc = plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, P.cap_stream);
+    hipGraph_t g = nullptr;
+    const hipError_t ce = hipStreamEndCapture(P.cap_stream, &g);
+    if (rc != TQ_OK) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    TQ_HIP(ce);
+    P.graph = g;
+    TQ_HIP(hipGraphInstantiate(&P.graph_exec, P.graph, nullptr, nullptr, 0));
+    P.gkey = key;
+    P.has_graph = true;
+    ++P.graph_builds;
+  }
+  TQ_HIP(hipGraphLaunch(P.graph_exec, stream));
+  ++P.graph_launches;
+  return TQ_OK;
+}
+
+int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
+                 int64_t s_step, int accumulate, hipStream_t stream) {
   const size_t esz = P.esz;
   std::vector<int64_t> in_off(P.n_inputs, 0);
   const int ns = (int)P.sliced.size();

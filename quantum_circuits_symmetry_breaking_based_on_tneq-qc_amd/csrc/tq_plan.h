@@ -80,6 +80,24 @@ struct Plan {
   double flops_slice = 0, bytes_slice = 0;  // per slice
   int n_gemm = 0, n_apply = 0, n_permute = 0;
   std::string describe;
+  // hipGraph of the whole launch sequence of one execute call, replayed while the call's
+  // pointers / slice range / flags are unchanged (a plan is hundreds of small launches)
+  struct GraphKey {
+    std::vector<const void*> inputs;
+    void* out = nullptr;
+    int64_t b = 0, e = 0, s = 0;
+    int acc = 0;
+    bool operator==(const GraphKey& o) const {
+      return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc;
+    }
+  };
+  bool use_graph = true;
+  bool has_graph = false;
+  GraphKey gkey;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  hipStream_t cap_stream = nullptr;
+  int64_t graph_builds = 0, graph_launches = 0;
 };
 
 int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, const int32_t* in_modes,
