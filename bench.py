@@ -151,7 +151,7 @@ def main():
     plan.profile(-1)
     step()
     torch.cuda.synchronize()
-    kinds = {k: plan.profile_read(getattr(_lib, f"TQ_OP_{k}")) for k in ("APPLY", "PERMUTE", "GEMM")}
+    kinds = {k: plan.profile_read(getattr(_lib, f"TQ_OP_{k}")) for k in ("APPLY", "SWEEP", "PERMUTE", "GEMM")}
     plan.profile(None)
 
     n_amp = task.n_amplitudes
@@ -160,6 +160,7 @@ def main():
     gemm_flops = gemm["flops"] / max(1, gemm["launches"])
     achieved = gemm_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     apply_ = kinds["APPLY"]
+    sweep_ = kinds["SWEEP"]
     res = {
         "metric": "amplitudes/sec + achieved MFMA TFLOP/s, 53q depth-20 RQC",
         "value": value,
@@ -198,6 +199,9 @@ def main():
         "hbm_kernels": {
             "apply_GBps": (apply_["bytes"] / (apply_["ms"] / 1e3) / 1e9) if apply_["ms"] else None,
             "apply_ms_per_step": apply_["ms"],
+            "sweep_GBps": (sweep_["bytes"] / (sweep_["ms"] / 1e3) / 1e9) if sweep_["ms"] else None,
+            "sweep_ms_per_step": sweep_["ms"],
+            "sweep_launches_per_step": sweep_["launches"],
             "permute_ms_per_step": kinds["PERMUTE"]["ms"],
             "gemm_ms_per_step": kinds["GEMM"]["ms"],
             "peak_GBps": PEAK_HBM_GBS,

@@ -124,7 +124,7 @@ int tq_plan_destroy(tq_plan plan);
  * 0 = off).  tq_plan_profile_read sums, over the launches of one
  * op kind since the reset (TQ_OP_PERMUTE / TQ_OP_GEMM / TQ_OP_APPLY, or -1 for all), the
  * elapsed milliseconds, the launch count and the algorithmic flops / bytes. */
-enum { TQ_OP_PERMUTE = 0, TQ_OP_GEMM = 1, TQ_OP_APPLY = 2, TQ_OP_AXPY = 3 };
+enum { TQ_OP_PERMUTE = 0, TQ_OP_GEMM = 1, TQ_OP_APPLY = 2, TQ_OP_AXPY = 3, TQ_OP_SWEEP = 4 };
 int tq_plan_profile(tq_plan plan, int enable);
 int tq_plan_profile_read(tq_plan plan, int op_kind, double* total_ms, int64_t* launches,
                          double* flops, double* bytes);

@@ -24,7 +24,7 @@ EXPORTED = (
     "tq_plan_create", "tq_plan_query", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
     "tq_plan_profile", "tq_plan_profile_read",
 )
-TQ_OP_PERMUTE, TQ_OP_GEMM, TQ_OP_APPLY, TQ_OP_AXPY = 0, 1, 2, 3
+TQ_OP_PERMUTE, TQ_OP_GEMM, TQ_OP_APPLY, TQ_OP_AXPY, TQ_OP_SWEEP = 0, 1, 2, 3, 4
 
 
 class TneqHipError(RuntimeError):

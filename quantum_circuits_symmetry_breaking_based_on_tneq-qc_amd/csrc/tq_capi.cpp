@@ -167,6 +167,8 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;
   if (k == "n_permute") return P.n_permute;
+  if (k == "n_sweep") return P.n_sweep;
+  if (k == "n_sweep_gates") return P.n_sweep_gates;
   if (k == "out_numel") return P.out_numel;
   return -1;
 }

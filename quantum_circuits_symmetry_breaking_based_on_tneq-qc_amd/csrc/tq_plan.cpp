@@ -18,8 +18,10 @@
 // from the input views, each slice only shifts input base pointers; slices are summed into the
 // output by the final op's beta.
 #include "tq_plan.h"
+#include "tq_sweep.h"
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -103,6 +105,7 @@ class Compiler {
     P_.esz = dtype_size(P_.dtype);
     cplx_ = dtype_complex(P_.dtype);
     P_.n_inputs = n_inputs;
+    n_inputs_ = n_inputs;
     std::set<int> sl(sliced, sliced + n_sliced);
     TQ_CHECK_ARG((int)sl.size() == n_sliced, "duplicate sliced mode");
     P_.sliced.assign(sliced, sliced + n_sliced);
@@ -176,6 +179,23 @@ class Compiler {
         }
       }
     }
+    // ---- branches: the two subtrees of the final step are independent (run concurrently)
+    step_branch_.assign(n_steps, 0);
+    if (n_steps >= 1) {
+      const int last = n_steps - 1;
+      step_branch_[last] = 2;
+      for (int side = 0; side < 2; ++side) {
+        std::vector<int> stack{path[2 * last + side]};
+        while (!stack.empty()) {
+          const int id = stack.back();
+          stack.pop_back();
+          if (id < n_inputs || id - n_inputs >= last) continue;
+          step_branch_[id - n_inputs] = side;
+          stack.push_back(path[2 * (id - n_inputs)]);
+          stack.push_back(path[2 * (id - n_inputs) + 1]);
+        }
+      }
+    }
     // ---- steps
     std::vector<bool> used(n_inputs + n_steps, false);
     for (int s = 0; s < n_steps; ++s) {
@@ -186,9 +206,11 @@ class Compiler {
       used[x] = used[y] = true;
       Live res;
       pin_next_ = pinned_[nid];
+      br_ = step_branch_[s];
       TQ_TRY(step(s, live_[x], live_[y], s == n_steps - 1, res));
       live_.push_back(res);
     }
+    TQ_TRY(flush_chain(false));  // (the final step always closes a chain; kept for safety)
     int remaining = 0, last = -1;
     for (int i = 0; i < n_inputs + n_steps; ++i) if (!used[i]) { ++remaining; last = i; }
     TQ_CHECK_ARG(remaining == 1, "path does not reduce to a single tensor");
@@ -199,8 +221,24 @@ class Compiler {
         TQ_CHECK_ARG(outset.count(m), "single-input trace/sum is unsupported");
       TQ_TRY(emit_permute(L, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, -1, "copy->out"));
     }
-    P_.pinned_base = (size_t)((arena_.peak() + kAlign - 1) / kAlign * kAlign);
-    P_.arena_bytes = P_.pinned_base + (size_t)pinned_arena_.peak();
+    // arena layout: [region 0][region 1] | pinned: [region 0][region 1]; offsets become absolute
+    {
+      auto al = [](int64_t b) { return (b + kAlign - 1) / kAlign * kAlign; };
+      const int64_t abase[2] = {0, al(arenas_[0].peak())};
+      const int64_t pbase[2] = {0, al(pinned_arenas_[0].peak())};
+      P_.pinned_base = (size_t)al(abase[1] + arenas_[1].peak());
+      P_.arena_bytes = P_.pinned_base + (size_t)(pbase[1] + pinned_arenas_[1].peak());
+      const int64_t esz = (int64_t)P_.esz;
+      auto fix = [&](BufRef& b) {
+        if (b.kind == BUF_ARENA) b.off += abase[b.region] / esz;
+        else if (b.kind == BUF_PINNED) b.off += pbase[b.region] / esz;
+        b.region = 0;
+      };
+      for (auto& op : P_.ops) {
+        fix(op.a); fix(op.b); fix(op.c); fix(op.ws);
+        for (auto& g : op.sgates) fix(g.g);
+      }
+    }
     // table layout
     size_t tb = 0;
     P_.perm_tab_off.clear();
@@ -213,6 +251,11 @@ class Compiler {
       P_.gtab_off.push_back(tb);
       tb += (g.size() * sizeof(int32_t) + kAlign - 1) / kAlign * kAlign;
     }
+    P_.stab_off.clear();
+    for (auto& b : P_.stabs) {
+      P_.stab_off.push_back(tb);
+      tb += (b.size() + kAlign - 1) / kAlign * kAlign;
+    }
     P_.table_bytes = tb;
     for (auto& op : P_.ops) {
       (op.invariant ? P_.flops_once : P_.flops_slice) += op.flops;
@@ -220,12 +263,15 @@ class Compiler {
       P_.n_gemm += op.kind == OP_GEMM;
       P_.n_apply += op.kind == OP_APPLY;
       P_.n_permute += op.kind == OP_PERMUTE;
+      P_.n_sweep += op.kind == OP_SWEEP;
+      if (op.kind == OP_SWEEP) P_.n_sweep_gates += (int)op.sgates.size();
     }
     P_.flops = P_.flops_once + P_.flops_slice * (double)P_.n_slices;
     P_.bytes = P_.bytes_once + P_.bytes_slice * (double)P_.n_slices;
     std::ostringstream d;
     for (size_t i = 0; i < P_.ops.size(); ++i)
-      d << (P_.ops[i].invariant ? "[once]  " : "[slice] ") << P_.ops[i].note << "\n";
+      d << (P_.ops[i].invariant ? "[once]  " : "[slice] ") << "b" << P_.ops[i].branch << " "
+        << P_.ops[i].note << "\n";
     P_.describe = d.str();
     return TQ_OK;
   }
@@ -241,25 +287,28 @@ class Compiler {
     return TQ_OK;
   }
 
+  int region() const { return br_ == 1 ? 1 : 0; }
   BufRef new_buf(int64_t numel, int64_t* off_out) {
-    const int64_t off = arena_.alloc(numel * (int64_t)P_.esz);
+    const int64_t off = arenas_[region()].alloc(numel * (int64_t)P_.esz);
     *off_out = off;
     BufRef b;
     b.kind = BUF_ARENA;
     b.off = off / (int64_t)P_.esz;
+    b.region = region();
     return b;
   }
   void release(const Live& L) {
-    if (L.owned && L.buf.kind == BUF_ARENA) arena_.release(L.buf.off * (int64_t)P_.esz);
+    if (L.owned && L.buf.kind == BUF_ARENA) arenas_[L.buf.region].release(L.buf.off * (int64_t)P_.esz);
   }
   // the step result's buffer: pinned results live in the separate pinned region
   BufRef new_result_buf(int64_t numel, int64_t* off_out) {
     if (!pin_next_) return new_buf(numel, off_out);
-    const int64_t off = pinned_arena_.alloc(numel * (int64_t)P_.esz);
+    const int64_t off = pinned_arenas_[region()].alloc(numel * (int64_t)P_.esz);
     *off_out = off;
     BufRef b;
     b.kind = BUF_PINNED;
     b.off = off / (int64_t)P_.esz;
+    b.region = region();
     return b;
   }
 
@@ -329,17 +378,89 @@ class Compiler {
       else (need ? freeA : sumA).insert(m);
     }
     for (int m : B0.modes) if (!inA.count(m)) (cnt_[m] > 0 ? freeB : sumB).insert(m);
+    const bool dep = A0.dep || B0.dep;
+    const int nid = n_inputs_ + s;
 
+    ApplyDesc d;
+    const bool can_apply = apply_desc(A0, B0, batch, contr, sumA, sumB, d);
+    // ---- fused sweep chains: an APPLY whose big operand is the open chain's result extends it
+    if (chain_.active) {
+      const bool pendA = A0.buf.kind == BUF_PENDING, pendB = B0.buf.kind == BUF_PENDING;
+      bool extended = false;
+      if (can_apply && (d.a_big ? pendA : pendB) && !(d.a_big ? pendB : pendA) && dep == chain_.dep &&
+          br_ == chain_.br) {
+        Chain::Gate g = make_gate(s, d, d.a_big ? B0 : A0, d.a_big ? A0 : B0, dep);
+        chain_.gates.push_back(g);
+        ChainShape sh;
+        if (sweeps_enabled() && chain_shape(chain_, d.order, sh)) {
+          chain_.out_modes = d.order;
+          chain_.id = nid;
+          extended = true;
+        } else {
+          chain_.gates.pop_back();
+        }
+      }
+      if (!extended) {
+        TQ_TRY(flush_chain(false));
+        // the flushed result now has a real buffer: refresh this step's copies
+        if (A0.buf.kind == BUF_PENDING) A0 = live_[chain_.flushed_id];
+        if (B0.buf.kind == BUF_PENDING) B0 = live_[chain_.flushed_id];
+      } else {
+        res.modes = d.order;
+        for (int m : d.order) res.ext.push_back(ext_[m]);
+        res.stride = contig_strides(res.ext);
+        res.buf = BufRef{BUF_PENDING, nid, 0};
+        res.owned = true;
+        res.dep = dep;
+        for (int m : res.modes) cnt_[m]++;
+        if (final) {
+          live_.push_back(res);  // flush patches live_[id]; the caller's push is replaced below
+          TQ_TRY(flush_chain(true));
+          res = live_.back();
+          live_.pop_back();
+        }
+        return TQ_OK;
+      }
+    }
     const size_t first_op = P_.ops.size();
-    int rc = TQ_OK;
-    const bool applied = try_apply(s, A0, B0, final, batch, contr, sumA, sumB, res, rc);
-    if (rc != TQ_OK) return rc;
-    if (!applied) TQ_TRY(gemm_step(s, A0, B0, final, batch, contr, freeA, freeB, sumA, sumB, res));
+    if (can_apply && !final && sweeps_enabled() && A0.buf.kind != BUF_PENDING &&
+        B0.buf.kind != BUF_PENDING) {
+      // open a chain with this gate (emitted at flush: as APPLY if it stays a single gate)
+      chain_ = Chain{};
+      chain_.active = true;
+      chain_.dep = dep;
+      chain_.br = br_;
+      chain_.X0 = d.a_big ? A0 : B0;
+      chain_.release_X0 = !(dep && !chain_.X0.dep);
+      chain_.gates.push_back(make_gate(s, d, d.a_big ? B0 : A0, d.a_big ? A0 : B0, dep));
+      chain_.out_modes = d.order;
+      chain_.id = nid;
+      ChainShape sh;
+      if (chain_shape(chain_, d.order, sh)) {
+        res.modes = d.order;
+        for (int m : d.order) res.ext.push_back(ext_[m]);
+        res.stride = contig_strides(res.ext);
+        res.buf = BufRef{BUF_PENDING, nid, 0};
+        res.owned = true;
+        res.dep = dep;
+        for (int m : res.modes) cnt_[m]++;
+        return TQ_OK;
+      }
+      chain_ = Chain{};  // does not fit a sweep tile: plain APPLY below
+    }
+    if (can_apply) {
+      TQ_TRY(emit_apply(s, d, final, A0, B0, res));
+    } else {
+      TQ_TRY(gemm_step(s, A0, B0, final, batch, contr, freeA, freeB, sumA, sumB, res));
+    }
     for (int m : res.modes) cnt_[m]++;
     // slice-invariant hoisting: a step that reads no sliced input runs once per execute; its
     // result is pinned in the arena when a slice-dependent step consumes it
-    res.dep = A0.dep || B0.dep;
-    for (size_t k = first_op; k < P_.ops.size(); ++k) P_.ops[k].invariant = !res.dep;
+    res.dep = dep;
+    for (size_t k = first_op; k < P_.ops.size(); ++k) {
+      P_.ops[k].invariant = !res.dep;
+      P_.ops[k].branch = br_;
+    }
     if (!(res.dep && !A0.dep)) release(A0);
     if (!(res.dep && !B0.dep)) release(B0);
     return TQ_OK;
@@ -354,18 +475,26 @@ class Compiler {
     return new_result_buf(numel, off);
   }
 
-  bool try_apply(int s, const Live& A0, const Live& B0, bool final, const std::set<int>& batch,
-                 const std::set<int>& contr, const std::set<int>& sumA, const std::set<int>& sumB,
-                 Live& res, int& rc) {
+  // ---- APPLY lowering: big operand S = [O][K1][M][K2][I] (contracted modes in <= 2 runs),
+  // small operand G[K][N] read through a gather table, C = [O][N][M][I]
+  struct ApplyDesc {
+    bool a_big = true;
+    std::vector<int> korder, nfree, order;
+    int64_t O = 1, K1 = 1, M = 1, K2 = 1, I = 1, K = 1, N = 1;
+    std::vector<int32_t> gtab;   // empty: small operand already contiguous in [K][N] order
+  };
+
+  bool apply_desc(const Live& A0, const Live& B0, const std::set<int>& batch,
+                  const std::set<int>& contr, const std::set<int>& sumA, const std::set<int>& sumB,
+                  ApplyDesc& d) {
     if (!batch.empty() || !sumA.empty() || !sumB.empty() || contr.empty()) return false;
-    const bool a_big = A0.numel() >= B0.numel();
-    const Live& Bg = a_big ? A0 : B0;
-    const Live& Sm = a_big ? B0 : A0;
-    if (!Bg.contiguous()) return false;
-    const int64_t K = ext_of(std::vector<int>(contr.begin(), contr.end()));
-    const int64_t N = Sm.numel() / K;
-    if (Sm.numel() > 1024 || K > 32 || N > 32) return false;
-    // contracted modes must form at most two runs in the big operand: [O][K1][M][K2][I]
+    d.a_big = A0.numel() >= B0.numel();
+    const Live& Bg = d.a_big ? A0 : B0;
+    const Live& Sm = d.a_big ? B0 : A0;
+    if (Bg.buf.kind != BUF_PENDING && !Bg.contiguous()) return false;
+    d.K = ext_of(std::vector<int>(contr.begin(), contr.end()));
+    d.N = Sm.numel() / d.K;
+    if (Sm.numel() > 1024 || d.K > 32 || d.N > 32) return false;
     std::vector<std::pair<int, int>> runs;  // (start, length)
     for (int i = 0; i < (int)Bg.modes.size(); ++i) {
       if (!contr.count(Bg.modes[i])) continue;
@@ -376,78 +505,330 @@ class Compiler {
     const int p1 = runs[0].first, c1 = runs[0].second;
     const int p2 = runs.size() == 2 ? runs[1].first : p1 + c1;
     const int c2 = runs.size() == 2 ? runs[1].second : 0;
-    std::vector<int> korder(Bg.modes.begin() + p1, Bg.modes.begin() + p1 + c1);
-    korder.insert(korder.end(), Bg.modes.begin() + p2, Bg.modes.begin() + p2 + c2);
-    std::vector<int> nfree;
-    for (int m : Sm.modes) if (!contr.count(m)) nfree.push_back(m);
-    // small operand read as G[K][N] through a gather table (any layout / strides, no launch)
-    int gtab = -1;
-    {
-      std::vector<int> gorder = korder;
-      gorder.insert(gorder.end(), nfree.begin(), nfree.end());
-      if (!(Sm.contiguous() && Sm.modes == gorder)) {
-        std::vector<int64_t> gext, gst;
-        for (int m : gorder) {
-          const int p = Sm.pos(m);
-          gext.push_back(Sm.ext[p]);
-          gst.push_back(Sm.stride[p]);
-        }
-        const int64_t n = prod(gext);
-        std::vector<int32_t> tab(n);
-        for (int64_t t = 0; t < n; ++t) {
-          int64_t rem = t, off = 0;
-          for (int d = (int)gext.size() - 1; d >= 0; --d) { off += (rem % gext[d]) * gst[d]; rem /= gext[d]; }
-          tab[t] = (int32_t)off;
-        }
-        gtab = (int)P_.gtabs.size();
-        P_.gtabs.push_back(std::move(tab));
+    d.korder.assign(Bg.modes.begin() + p1, Bg.modes.begin() + p1 + c1);
+    d.korder.insert(d.korder.end(), Bg.modes.begin() + p2, Bg.modes.begin() + p2 + c2);
+    for (int m : Sm.modes) if (!contr.count(m)) d.nfree.push_back(m);
+    std::vector<int> gorder = d.korder;
+    gorder.insert(gorder.end(), d.nfree.begin(), d.nfree.end());
+    if (!(Sm.contiguous() && Sm.modes == gorder)) {
+      std::vector<int64_t> gext, gst;
+      for (int m : gorder) {
+        const int p = Sm.pos(m);
+        gext.push_back(Sm.ext[p]);
+        gst.push_back(Sm.stride[p]);
+      }
+      const int64_t n = prod(gext);
+      d.gtab.resize(n);
+      for (int64_t t = 0; t < n; ++t) {
+        int64_t rem = t, off = 0;
+        for (int q = (int)gext.size() - 1; q >= 0; --q) { off += (rem % gext[q]) * gst[q]; rem /= gext[q]; }
+        d.gtab[t] = (int32_t)off;
       }
     }
-    std::vector<int> order(Bg.modes.begin(), Bg.modes.begin() + p1);
-    order.insert(order.end(), nfree.begin(), nfree.end());
-    order.insert(order.end(), Bg.modes.begin() + p1 + c1, Bg.modes.begin() + p2);
-    order.insert(order.end(), Bg.modes.begin() + p2 + c2, Bg.modes.end());
-    int64_t O = 1, K1 = 1, M = 1, K2 = 1, I = 1;
-    for (int i = 0; i < p1; ++i) O *= Bg.ext[i];
-    for (int i = p1; i < p1 + c1; ++i) K1 *= Bg.ext[i];
-    for (int i = p1 + c1; i < p2; ++i) M *= Bg.ext[i];
-    for (int i = p2; i < p2 + c2; ++i) K2 *= Bg.ext[i];
-    for (size_t i = p2 + c2; i < Bg.modes.size(); ++i) I *= Bg.ext[i];
-    const int64_t outn = O * N * M * I;
+    d.order.assign(Bg.modes.begin(), Bg.modes.begin() + p1);
+    d.order.insert(d.order.end(), d.nfree.begin(), d.nfree.end());
+    d.order.insert(d.order.end(), Bg.modes.begin() + p1 + c1, Bg.modes.begin() + p2);
+    d.order.insert(d.order.end(), Bg.modes.begin() + p2 + c2, Bg.modes.end());
+    for (int i = 0; i < p1; ++i) d.O *= Bg.ext[i];
+    for (int i = p1; i < p1 + c1; ++i) d.K1 *= Bg.ext[i];
+    for (int i = p1 + c1; i < p2; ++i) d.M *= Bg.ext[i];
+    for (int i = p2; i < p2 + c2; ++i) d.K2 *= Bg.ext[i];
+    for (size_t i = p2 + c2; i < Bg.modes.size(); ++i) d.I *= Bg.ext[i];
+    return true;
+  }
+
+  int add_gtab(const std::vector<int32_t>& t) {
+    if (t.empty()) return -1;
+    P_.gtabs.push_back(t);
+    return (int)P_.gtabs.size() - 1;
+  }
+
+  int emit_apply(int s, const ApplyDesc& d, bool final, const Live& A0, const Live& B0, Live& res) {
+    const Live& Bg = d.a_big ? A0 : B0;
+    const Live& Sm = d.a_big ? B0 : A0;
+    const int64_t outn = d.O * d.N * d.M * d.I;
     bool direct;
     int64_t roff;
-    BufRef tgt = result_target(final, order, outn, &direct, &roff);
+    BufRef tgt = result_target(final, d.order, outn, &direct, &roff);
     Op op;
     op.kind = OP_APPLY;
     op.a = Bg.buf;
     op.b = Sm.buf;
-    op.gtab = gtab;
+    op.gtab = add_gtab(d.gtab);
     op.c = tgt;
     op.writes_output = direct;
-    op.O = O; op.K = K1; op.M = M; op.K2 = K2; op.N = N; op.I = I;
+    op.O = d.O; op.K = d.K1; op.M = d.M; op.K2 = d.K2; op.N = d.N; op.I = d.I;
     op.step = s;
-    op.flops = (double)O * M * I * K * N * (cplx_ ? 8.0 : 2.0);
-    op.bytes = (double)(O * K * M * I + outn + K * N) * P_.esz;
+    op.flops = (double)d.O * d.M * d.I * d.K * d.N * (cplx_ ? 8.0 : 2.0);
+    op.bytes = (double)(d.O * d.K * d.M * d.I + outn + d.K * d.N) * P_.esz;
     std::ostringstream o;
-    o << "step " << s << " APPLY O=" << O << " K1=" << K1 << " M=" << M << " K2=" << K2
-      << " I=" << I << " N=" << N << (direct ? " ->OUT" : "");
+    o << "step " << s << " APPLY O=" << d.O << " K1=" << d.K1 << " M=" << d.M << " K2=" << d.K2
+      << " I=" << d.I << " N=" << d.N << (direct ? " ->OUT" : "");
     op.note = o.str();
     P_.ops.push_back(op);
-    res.modes = order;
-    for (int m : order) res.ext.push_back(ext_[m]);
+    res.modes = d.order;
+    res.ext.clear();
+    for (int m : d.order) res.ext.push_back(ext_[m]);
     res.stride = contig_strides(res.ext);
-    if (direct) {
-      res.buf = tgt;
-      res.owned = false;
-    } else {
-      res.buf = tgt;
-      res.owned = true;
-      if (final) {
-        rc = emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, s, "result->out");
-        if (rc != TQ_OK) return true;
-      }
+    res.buf = tgt;
+    res.owned = !direct;
+    if (final && !direct)
+      TQ_TRY(emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, s, "result->out"));
+    return TQ_OK;
+  }
+
+  // ---- sweep chains ------------------------------------------------------------------------
+  struct Chain {
+    struct Gate {
+      Live Sm;
+      bool release = true;
+      int step = -1;
+      ApplyDesc d;
+    };
+    bool active = false;
+    bool dep = false;
+    int br = 0;           // branch of its steps
+    int id = -1;          // SSA id of the (pending) chain result
+    int flushed_id = -1;
+    Live X0;
+    bool release_X0 = true;
+    std::vector<Gate> gates;
+    std::vector<int> out_modes;
+  };
+  struct ChainShape {
+    std::vector<int> tin, tout, outer;
+    std::vector<std::vector<int>> W;   // working-set mode lists after each gate (W[q-1] = tout)
+    int64_t tin_n = 1, tout_n = 1, wmax = 1;
+  };
+
+  static bool sweeps_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_SWEEP");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
+
+  Chain::Gate make_gate(int s, const ApplyDesc& d, const Live& Sm, const Live& Bg, bool dep) {
+    Chain::Gate g;
+    g.Sm = Sm;
+    g.step = s;
+    g.d = d;
+    (void)Bg;
+    g.release = !(dep && !Sm.dep);
+    return g;
+  }
+
+  int64_t count_of(const std::vector<int>& ms) { return ext_of(ms); }
+
+  // tile modes / working sets of a chain; false if it does not fit the sweep kernel's limits
+  bool chain_shape(const Chain& c, const std::vector<int>& out_modes, ChainShape& sh) {
+    if ((int)c.gates.size() > kSweepMaxGates) return false;
+    std::set<int> contracted;
+    for (auto& g : c.gates) {
+      if (g.d.K * g.d.N > kSweepMaxKN) return false;
+      contracted.insert(g.d.korder.begin(), g.d.korder.end());
     }
-    return true;
+    for (int m : c.X0.modes) (contracted.count(m) ? sh.tin : sh.outer).push_back(m);
+    std::vector<int> w = sh.tin;
+    sh.W.clear();
+    for (size_t j = 0; j < c.gates.size(); ++j) {
+      const auto& g = c.gates[j];
+      std::vector<int> nw;
+      for (int m : w) if (std::find(g.d.korder.begin(), g.d.korder.end(), m) == g.d.korder.end()) nw.push_back(m);
+      for (int m : g.d.korder)
+        if (std::find(w.begin(), w.end(), m) == w.end()) return false;  // contracts an outer mode
+      nw.insert(nw.end(), g.d.nfree.begin(), g.d.nfree.end());
+      w = nw;
+      sh.W.push_back(w);
+      sh.wmax = std::max(sh.wmax, count_of(w));
+    }
+    std::set<int> wset(w.begin(), w.end());
+    for (int m : out_modes) if (wset.count(m)) sh.tout.push_back(m);
+    if (sh.tout.size() != w.size()) return false;
+    sh.W.back() = sh.tout;
+    // untouched modes keep their relative order (APPLY preserves it)
+    std::vector<int> outer_y;
+    for (int m : out_modes) if (!wset.count(m)) outer_y.push_back(m);
+    if (outer_y != sh.outer) return false;
+    sh.tin_n = count_of(sh.tin);
+    sh.tout_n = count_of(sh.tout);
+    sh.wmax = std::max({sh.wmax, sh.tin_n, sh.tout_n});
+    int64_t tab = 0;
+    for (size_t j = 0; j < c.gates.size(); ++j) tab += count_of(sh.W[j]) * (c.gates[j].d.K + 1);
+    return sh.wmax <= sweep_wmax((int)P_.esz) && tab <= kSweepTabMax;
+  }
+
+  // mixed-radix digits of index t over `modes` (last fastest)
+  void digits(int64_t t, const std::vector<int>& modes, std::map<int, int64_t>& dig) {
+    for (int q = (int)modes.size() - 1; q >= 0; --q) {
+      const int64_t e = ext_[modes[q]];
+      dig[modes[q]] = t % e;
+      t /= e;
+    }
+  }
+  int64_t index_of(const std::vector<int>& modes, const std::map<int, int64_t>& dig) {
+    int64_t t = 0;
+    for (int m : modes) t = t * ext_[m] + dig.at(m);
+    return t;
+  }
+
+  int flush_chain(bool final) {
+    if (!chain_.active) return TQ_OK;
+    Chain c = chain_;
+    chain_ = Chain{};
+    chain_.flushed_id = c.id;
+    const size_t first_op = P_.ops.size();
+    Live res;
+    const bool saved_pin = pin_next_;
+    const int saved_br = br_;
+    pin_next_ = pinned_[c.id];
+    br_ = c.br;
+    if (c.gates.size() == 1) {
+      const auto& g = c.gates[0];
+      const Live& A0 = g.d.a_big ? c.X0 : g.Sm;
+      const Live& B0 = g.d.a_big ? g.Sm : c.X0;
+      TQ_TRY(emit_apply(g.step, g.d, final, A0, B0, res));
+    } else {
+      ChainShape sh;
+      if (!chain_shape(c, c.out_modes, sh)) { set_error("internal: chain shape"); return TQ_ERR_INVALID; }
+      const int64_t n0 = c.X0.numel();
+      const int64_t nq = n0 / sh.tin_n * sh.tout_n;
+      bool direct;
+      int64_t roff;
+      BufRef tgt = result_target(final, c.out_modes, nq, &direct, &roff);
+      Op op;
+      op.kind = OP_SWEEP;
+      op.a = c.X0.buf;
+      op.c = tgt;
+      op.writes_output = direct;
+      op.step = c.gates.back().step;
+      op.tin = (int)sh.tin_n;
+      op.tout = (int)sh.tout_n;
+      op.ncols = n0 / sh.tin_n;
+      // strides of X0 (contiguous, its own order) and of Y (contiguous, out order)
+      std::map<int, int64_t> sx, sy;
+      {
+        auto cs = contig_strides(c.X0.ext);
+        for (size_t q = 0; q < c.X0.modes.size(); ++q) sx[c.X0.modes[q]] = cs[q];
+        std::vector<int64_t> ye;
+        for (int m : c.out_modes) ye.push_back(ext_[m]);
+        auto cy = contig_strides(ye);
+        for (size_t q = 0; q < c.out_modes.size(); ++q) sy[c.out_modes[q]] = cy[q];
+      }
+      // outer runs (merge neighbours contiguous in both X and Y), innermost first
+      std::vector<std::array<int64_t, 3>> runs;  // ext, in stride, out stride (outer->inner)
+      for (int m : sh.outer) {
+        const int64_t e = ext_[m];
+        if (e == 1) continue;
+        if (!runs.empty() && runs.back()[1] == sx[m] * e && runs.back()[2] == sy[m] * e) {
+          runs.back()[0] *= e;
+          runs.back()[1] = sx[m];
+          runs.back()[2] = sy[m];
+        } else {
+          runs.push_back({e, sx[m], sy[m]});
+        }
+      }
+      if (runs.size() > (size_t)kSweepMaxRuns) { set_error("internal: sweep runs"); return TQ_ERR_INVALID; }
+      std::reverse(runs.begin(), runs.end());
+      op.nruns = (int)runs.size();
+      for (size_t r = 0; r < runs.size(); ++r) {
+        op.run_ext[r] = runs[r][0]; op.run_in[r] = runs[r][1]; op.run_out[r] = runs[r][2];
+      }
+      // tables: tin_off (int64) | tout_off (int64) | per gate [W][K+1] int16
+      std::vector<char> blob;
+      auto put64 = [&](int64_t v) { const char* p = (const char*)&v; blob.insert(blob.end(), p, p + 8); };
+      std::map<int, int64_t> dig;
+      for (int64_t t = 0; t < sh.tin_n; ++t) {
+        digits(t, sh.tin, dig);
+        int64_t o = 0;
+        for (int m : sh.tin) o += dig[m] * sx[m];
+        put64(o);
+      }
+      op.tout_off_at = blob.size();
+      for (int64_t t = 0; t < sh.tout_n; ++t) {
+        digits(t, sh.tout, dig);
+        int64_t o = 0;
+        for (int m : sh.tout) o += dig[m] * sy[m];
+        put64(o);
+      }
+      std::vector<int> prev = sh.tin;
+      double flops = 0;
+      op.tabs_at = blob.size();
+      size_t entries = 0;
+      for (size_t j = 0; j < c.gates.size(); ++j) {
+        const auto& g = c.gates[j];
+        const std::vector<int>& w = sh.W[j];
+        SweepGate sg;
+        sg.g = g.Sm.buf;
+        sg.gtab = add_gtab(g.d.gtab);
+        sg.K = (int)g.d.K;
+        sg.N = (int)g.d.N;
+        sg.W = (int)count_of(w);
+        sg.tab_off = entries;
+        for (int64_t e = 0; e < sg.W; ++e) {
+          std::map<int, int64_t> de;
+          digits(e, w, de);
+          std::map<int, int64_t> dn;
+          for (int m : g.d.nfree) dn[m] = de[m];
+          const int64_t n = index_of(g.d.nfree, dn);
+          for (int64_t k = 0; k < sg.K; ++k) {
+            std::map<int, int64_t> dk = de;
+            std::map<int, int64_t> kd;
+            digits(k, g.d.korder, kd);
+            for (auto& kv : kd) dk[kv.first] = kv.second;
+            const int32_t v = (int32_t)index_of(prev, dk);
+            blob.insert(blob.end(), (const char*)&v, (const char*)&v + 4);
+          }
+          const int32_t nv = (int32_t)n;
+          blob.insert(blob.end(), (const char*)&nv, (const char*)&nv + 4);
+          entries += sg.K + 1;
+        }
+        flops += (double)op.ncols * sg.W * sg.K * (cplx_ ? 8.0 : 2.0);
+        op.sgates.push_back(sg);
+        prev = w;
+      }
+      op.tab_len = (int)entries;
+      op.stab = (int)P_.stabs.size();
+      P_.stabs.push_back(std::move(blob));
+      // coalescing: walk columns fastest when the innermost outer run is unit-stride
+      op.load_colfast = (op.nruns > 0 && op.run_in[0] == 1 && op.run_ext[0] >= 16) ? 1 : 0;
+      op.store_colfast = (op.nruns > 0 && op.run_out[0] == 1 && op.run_ext[0] >= 16) ? 1 : 0;
+      op.flops = flops;
+      op.bytes = (double)(n0 + nq) * P_.esz;
+      std::ostringstream o;
+      o << "step " << c.gates.front().step << ".." << op.step << " SWEEP gates=" << c.gates.size()
+        << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " runs=" << op.nruns
+        << (direct ? " ->OUT" : "");
+      op.note = o.str();
+      P_.ops.push_back(op);
+      res.modes = c.out_modes;
+      for (int m : c.out_modes) res.ext.push_back(ext_[m]);
+      res.stride = contig_strides(res.ext);
+      res.buf = tgt;
+      res.owned = !direct;
+      if (final && !direct)
+        TQ_TRY(emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, op.step, "result->out"));
+    }
+    for (size_t k = first_op; k < P_.ops.size(); ++k) {
+      P_.ops[k].invariant = !c.dep;
+      P_.ops[k].branch = c.br;
+    }
+    res.dep = c.dep;
+    // the pending result gets its real buffer
+    Live& L = live_[c.id];
+    L.buf = res.buf;
+    L.owned = res.owned;
+    L.modes = res.modes;
+    L.ext = res.ext;
+    L.stride = res.stride;
+    L.dep = c.dep;
+    // operands are released only now, after the result buffer was placed
+    if (c.release_X0) release(c.X0);
+    for (auto& g : c.gates) if (g.release) release(g.Sm);
+    pin_next_ = saved_pin;
+    br_ = saved_br;
+    return TQ_OK;
   }
 
   struct GemmChoice {
@@ -551,8 +932,8 @@ class Compiler {
     op.ws_bytes = gemm_workspace(P_.dtype, M, N, K, bsz);
     int64_t wsoff = -1;
     if (op.ws_bytes) {
-      wsoff = arena_.alloc((int64_t)op.ws_bytes);
-      op.ws = BufRef{BUF_ARENA, 0, wsoff / (int64_t)P_.esz};
+      wsoff = arenas_[region()].alloc((int64_t)op.ws_bytes);
+      op.ws = BufRef{BUF_ARENA, 0, wsoff / (int64_t)P_.esz, region()};
     }
     op.step = s;
     op.flops = (double)bsz * M * N * K * (cplx_ ? 8.0 : 2.0);
@@ -563,9 +944,9 @@ class Compiler {
       << (direct ? " ->OUT" : "");
     op.note = o.str();
     P_.ops.push_back(op);
-    if (wsoff >= 0) arena_.release(wsoff);
-    if (aoff >= 0) arena_.release(aoff);
-    if (boff >= 0) arena_.release(boff);
+    if (wsoff >= 0) arenas_[region()].release(wsoff);
+    if (aoff >= 0) arenas_[region()].release(aoff);
+    if (boff >= 0) arenas_[region()].release(boff);
     res.modes = rord;
     for (int m : rord) res.ext.push_back(ext_[m]);
     res.stride = contig_strides(res.ext);
@@ -578,11 +959,15 @@ class Compiler {
 
   Plan& P_;
   bool cplx_ = false;
+  int n_inputs_ = 0;
+  Chain chain_;
   std::vector<Live> live_;
   std::map<int, int64_t> ext_;
   std::map<int, int> cnt_;
-  Arena arena_;
-  Arena pinned_arena_;
+  Arena arenas_[2];          // per branch, so the two subtrees can run concurrently
+  Arena pinned_arenas_[2];
+  int br_ = 0;               // branch of the step being compiled (0, 1, 2 = join)
+  std::vector<int> step_branch_;
   std::vector<char> pinned_;
   bool pin_next_ = false;
 };
@@ -606,6 +991,12 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
 }
 
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
+  if (!P.side_stream) TQ_HIP(hipStreamCreateWithFlags(&P.side_stream, hipStreamNonBlocking));
+  while (P.sync_events.size() < 2) {
+    hipEvent_t e;
+    TQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    P.sync_events.push_back(e);
+  }
   if (arena || tables) {
     P.d_arena = arena;
     P.d_tables = tables;
@@ -621,6 +1012,8 @@ int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
       if (perm_plan_table_bytes(P.perms[i])) perm_plan_pack_table(P.perms[i], host.data() + P.perm_tab_off[i]);
     for (size_t i = 0; i < P.gtabs.size(); ++i)
       std::memcpy(host.data() + P.gtab_off[i], P.gtabs[i].data(), P.gtabs[i].size() * sizeof(int32_t));
+    for (size_t i = 0; i < P.stabs.size(); ++i)
+      std::memcpy(host.data() + P.stab_off[i], P.stabs[i].data(), P.stabs[i].size());
     TQ_HIP(hipMemcpyAsync(P.d_tables, host.data(), P.table_bytes, hipMemcpyHostToDevice, stream));
     TQ_HIP(hipStreamSynchronize(stream));
   }
@@ -669,6 +1062,10 @@ void plan_release(Plan& P) {
   drop_graph(P);
   if (P.cap_stream) (void)hipStreamDestroy(P.cap_stream);
   P.cap_stream = nullptr;
+  if (P.side_stream) (void)hipStreamDestroy(P.side_stream);
+  P.side_stream = nullptr;
+  for (auto e : P.sync_events) (void)hipEventDestroy(e);
+  P.sync_events.clear();
   for (auto& ev : P.ev_used) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   for (auto& ev : P.ev_free) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   P.ev_used.clear();
@@ -727,7 +1124,18 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     if (!accumulate && P.out_numel) TQ_HIP(hipMemsetAsync(out, 0, P.out_numel * esz, stream));
     return TQ_OK;
   }
+  // the two independent subtrees of the final step run on two streams: branch-1 ops on the side
+  // stream, forked from `stream` at every slice start and joined before the first join op
+  bool two = false;
+  for (const Op& op : P.ops) two |= op.branch == 1;
+  two = two && P.side_stream != nullptr && P.sync_events.size() >= 2;
+  hipStream_t s1 = two ? P.side_stream : stream;
   for (int64_t sl = s_begin; sl < s_end; sl += s_step) {
+    bool joined = false;
+    if (two) {
+      TQ_HIP(hipEventRecord(P.sync_events[0], stream));
+      TQ_HIP(hipStreamWaitEvent(s1, P.sync_events[0], 0));
+    }
     // decode slice id (row-major over sliced modes) -> per-input element offsets
     std::vector<int64_t> idx(ns);
     int64_t rem = sl;
@@ -750,6 +1158,12 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     for (const Op& op : P.ops) {
       if (op.invariant && sl != s_begin) continue;  // hoisted: computed in this call's first slice
       const double beta = op.writes_output ? beta_out : 0.0;
+      if (two && op.branch == 2 && !joined) {
+        TQ_HIP(hipEventRecord(P.sync_events[1], s1));
+        TQ_HIP(hipStreamWaitEvent(stream, P.sync_events[1], 0));
+        joined = true;
+      }
+      hipStream_t st = op.branch == 1 ? s1 : stream;
       Plan::Ev ev{};
       const bool prof = (P.profile >> op.kind) & 1;
       if (prof) {
@@ -761,31 +1175,90 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           P.ev_free.pop_back();
         }
         ev.kind = op.kind; ev.flops = op.flops; ev.bytes = op.bytes;
-        TQ_HIP(hipEventRecord(ev.a, stream));
+        TQ_HIP(hipEventRecord(ev.a, st));
       }
       switch (op.kind) {
         case OP_PERMUTE:
           TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm],
-                                  ptr(op.a), ptr(op.c), beta, stream));
+                                  ptr(op.a), ptr(op.c), beta, st));
           break;
         case OP_GEMM:
           TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
                              op.lda, op.sA, ptr(op.b), op.ldb, op.sB, beta, ptr(op.c), op.ldc, op.sC,
-                             op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, stream));
+                             op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, st));
           break;
         case OP_APPLY:
           TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.M, op.K2, op.I, op.N, ptr(op.a), ptr(op.b),
                               op.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[op.gtab]) : nullptr,
-                              ptr(op.c), beta, stream));
+                              ptr(op.c), beta, st));
           break;
         case OP_AXPY:
-          TQ_TRY(axpy_launch(P.dtype, op.n, ptr(op.a), ptr(op.c), beta, stream));
+          TQ_TRY(axpy_launch(P.dtype, op.n, ptr(op.a), ptr(op.c), beta, st));
           break;
+        case OP_SWEEP: {
+          SweepArgs a;
+          const char* blob = (const char*)P.d_tables + P.stab_off[op.stab];
+          a.X = ptr(op.a);
+          a.Y = ptr(op.c);
+          a.ncols = op.ncols;
+          auto lg = [](int64_t v) {
+            if (v <= 0 || (v & (v - 1))) return -1;
+            int l = 0;
+            while ((int64_t(1) << l) < v) ++l;
+            return l;
+          };
+          a.nruns = op.nruns;
+          for (int r = 0; r < op.nruns; ++r) {
+            a.run_ext[r] = op.run_ext[r]; a.run_in[r] = op.run_in[r]; a.run_out[r] = op.run_out[r];
+            a.run_shift[r] = lg(op.run_ext[r]);
+          }
+          a.tin = op.tin;
+          a.tout = op.tout;
+          a.tin_shift = lg(op.tin);
+          a.tout_shift = lg(op.tout);
+          a.tabs = (const int32_t*)(blob + op.tabs_at);
+          a.tab_len = op.tab_len;
+          a.tin_off = (const int64_t*)blob;
+          a.tout_off = (const int64_t*)(blob + op.tout_off_at);
+          a.ngates = (int)op.sgates.size();
+          for (int j = 0; j < a.ngates; ++j) {
+            const SweepGate& g = op.sgates[j];
+            a.G[j] = ptr(g.g);
+            a.gidx[j] = g.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[g.gtab]) : nullptr;
+            a.K[j] = g.K; a.N[j] = g.N; a.W[j] = g.W;
+            a.tab_at[j] = (int)g.tab_off;
+          }
+          // power-of-two outer extents: per-bit column-offset weights
+          {
+            bool p2 = true;
+            int nb = 0;
+            for (int r = 0; r < op.nruns && p2; ++r) {
+              const int l = lg(op.run_ext[r]);
+              if (l < 0 || nb + l > 48) { p2 = false; break; }
+              for (int b = 0; b < l; ++b) {
+                a.w_in[nb + b] = op.run_in[r] << b;
+                a.w_out[nb + b] = op.run_out[r] << b;
+              }
+              nb += l;
+            }
+            a.colbits = p2 ? nb : -1;
+          }
+          a.load_colfast = op.load_colfast;
+          a.store_colfast = op.store_colfast;
+          a.use_beta = beta != 0.0;
+          a.beta = beta;
+          TQ_TRY(sweep_launch(P.dtype, a, st));
+          break;
+        }
       }
       if (prof) {
-        TQ_HIP(hipEventRecord(ev.b, stream));
+        TQ_HIP(hipEventRecord(ev.b, st));
         P.ev_used.push_back(ev);
       }
+    }
+    if (two && !joined) {
+      TQ_HIP(hipEventRecord(P.sync_events[1], s1));
+      TQ_HIP(hipStreamWaitEvent(stream, P.sync_events[1], 0));
     }
     first = false;
   }

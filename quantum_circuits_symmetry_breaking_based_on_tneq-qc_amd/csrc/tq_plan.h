@@ -10,20 +10,32 @@
 namespace tq {
 
 // where an operand lives
-enum BufKind { BUF_INPUT = 0, BUF_ARENA = 1, BUF_OUTPUT = 2, BUF_TABLE = 3, BUF_PINNED = 4 };
+enum BufKind { BUF_INPUT = 0, BUF_ARENA = 1, BUF_OUTPUT = 2, BUF_TABLE = 3, BUF_PINNED = 4,
+               BUF_PENDING = 5 /* compile time only: result of an open sweep chain */ };
 struct BufRef {
   int kind = BUF_ARENA;
   int64_t index = 0;  // input id for BUF_INPUT
   int64_t off = 0;    // element offset (bytes for BUF_TABLE)
+  int region = 0;     // compile time: arena region (branch) the offset is relative to
 };
 
-enum OpKind { OP_PERMUTE = 0, OP_GEMM = 1, OP_APPLY = 2, OP_AXPY = 3 };
+enum OpKind { OP_PERMUTE = 0, OP_GEMM = 1, OP_APPLY = 2, OP_AXPY = 3, OP_SWEEP = 4 };
+
+// one gate of a fused sweep op (OP_SWEEP): small operand + its gather table + index table
+struct SweepGate {
+  BufRef g;
+  int gtab = -1;
+  int K = 0, N = 0, W = 0;
+  size_t tab_off = 0;   // entry offset of its [W][K+1] int16 table in the op's packed tables
+};
 
 struct Op {
   int kind = OP_PERMUTE;
   BufRef a, b, c;       // permute: a -> c ; gemm: c = a*b ; apply: c = a (x) b ; axpy: c += a
   bool writes_output = false;
   bool invariant = false;  // reads no sliced input: run once per execute call (hoisted)
+  int branch = 0;          // 0 / 1: the two independent subtrees of the final step (run on two
+                           // streams concurrently); 2: the join (final step), after both
   // permute
   int perm = -1;        // index into Plan::perms
   // gemm
@@ -36,6 +48,17 @@ struct Op {
   int gtab = -1;         // gather table of the small operand (index into Plan::gtabs)
   // axpy
   int64_t n = 0;
+  // sweep (fused chain of APPLY steps): a = chain input, c = chain output, gates in order
+  std::vector<SweepGate> sgates;
+  int stab = -1;                 // index into Plan::stabs (tin_off | tout_off | gate tables)
+  int tin = 0, tout = 0;
+  int nruns = 0;
+  int64_t run_ext[8] = {}, run_in[8] = {}, run_out[8] = {};
+  int64_t ncols = 0;
+  size_t tout_off_at = 0;        // byte offset of tout_off inside the blob (tin_off at 0)
+  size_t tabs_at = 0;            // byte offset of the packed gate tables inside the blob
+  int tab_len = 0;
+  int load_colfast = 1, store_colfast = 1;
   // bookkeeping
   int step = -1;
   double flops = 0, bytes = 0;
@@ -65,6 +88,8 @@ struct Plan {
   std::vector<size_t> perm_tab_off;   // byte offset in the table buffer
   std::vector<std::vector<int32_t>> gtabs;  // APPLY small-operand gather tables
   std::vector<size_t> gtab_off;
+  std::vector<std::vector<char>> stabs;     // OP_SWEEP table blobs
+  std::vector<size_t> stab_off;
   size_t table_bytes = 0;
   size_t arena_bytes = 0;
   size_t pinned_base = 0;             // pinned (hoisted, slice-invariant) results live above this
@@ -78,7 +103,7 @@ struct Plan {
   double flops = 0, bytes = 0;              // whole execute (all slices)
   double flops_once = 0, bytes_once = 0;    // slice-invariant (hoisted) part
   double flops_slice = 0, bytes_slice = 0;  // per slice
-  int n_gemm = 0, n_apply = 0, n_permute = 0;
+  int n_gemm = 0, n_apply = 0, n_permute = 0, n_sweep = 0, n_sweep_gates = 0;
   std::string describe;
   // hipGraph of the whole launch sequence of one execute call, replayed while the call's
   // pointers / slice range / flags are unchanged (a plan is hundreds of small launches)
@@ -97,6 +122,8 @@ struct Plan {
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   hipStream_t cap_stream = nullptr;
+  hipStream_t side_stream = nullptr;        // branch-1 ops
+  std::vector<hipEvent_t> sync_events;      // fork / join events (reused)
   int64_t graph_builds = 0, graph_launches = 0;
 };
 

@@ -167,3 +167,57 @@ def test_graph_replay_matches_eager_and_rebuilds_on_new_pointers(dev):
     assert plan.query("graph_builds") == b0 + 2
     part0 = e(*ts, slice_range=(0, e.n_slices, 2))
     assert _err((part + part0).cpu().numpy(), ref) < TOL["complex64"]
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128", "float32", "float64"])
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_fused_sweep_chains_random(dev, dtype, seed):
+    """Random gate chains on a running tensor (binary and extent-3 legs, 1-2 contracted and
+    1-2 new legs per gate, inner and outer positions): the plan fuses consecutive absorptions
+    into SWEEP ops; the result equals the oracle's exact pairwise contraction."""
+    import torch
+    from tneq_qc_amd.expression import HipContractExpression
+    rng = np.random.default_rng(100 + seed)
+    syms = iter("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ")
+    ext = {}
+    cur = []
+    for _ in range(rng.integers(8, 13)):
+        s = next(syms)
+        ext[s] = 3 if rng.random() < 0.15 else 2
+        cur.append(s)
+    terms = ["".join(cur)]
+    for _ in range(rng.integers(6, 14)):
+        kc = int(rng.integers(1, 3))
+        pos = int(rng.integers(0, len(cur) - kc + 1))
+        contracted = cur[pos:pos + kc] if rng.random() < 0.7 else list(rng.choice(cur, kc, replace=False))
+        new = []
+        for _ in range(int(rng.integers(1, 3))):
+            s = next(syms)
+            ext[s] = 2
+            new.append(s)
+        terms.append("".join(contracted) + "".join(new))
+        cur = [c for c in cur if c not in contracted]
+        cur[pos:pos] = new
+    out = "".join(cur)
+    eq = ",".join(terms) + "->" + out
+    shapes = [tuple(ext[c] for c in t) for t in terms]
+    cplx = dtype.startswith("complex")
+    ops = []
+    for shp in shapes:
+        x = rng.standard_normal(shp)
+        if cplx:
+            x = x + 1j * rng.standard_normal(shp)
+        ops.append(x / np.sqrt(np.prod(shp[-2:]) if len(shp) > 1 else 1))
+    path = [(0, 1)] + [(len(terms) + i, i + 2) for i in range(len(terms) - 2)]
+    ref = ref_contract(eq, *ops)
+    e = HipContractExpression(eq, *shapes, optimize=path)
+    plan = e.plan(getattr(torch, dtype))
+    ts = [torch.from_numpy(np.ascontiguousarray(o)).to(dev, getattr(torch, dtype)) for o in ops]
+    got = e(*ts).cpu().numpy()
+    assert plan.query("n_sweep") >= 1, plan.describe()
+    tol = {"complex64": 2e-5, "float32": 2e-5, "complex128": 1e-12, "float64": 1e-12}[dtype]
+    assert _err(got, ref) < tol, plan.describe()
+    # accumulate (beta = 1) into an existing output
+    acc = torch.from_numpy(np.ascontiguousarray(ref)).to(dev, getattr(torch, dtype))
+    e(*ts, out=acc, accumulate=True)
+    assert _err(acc.cpu().numpy(), 2 * ref) < tol

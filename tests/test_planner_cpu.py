@@ -72,9 +72,13 @@ def _plan(task, dtype="complex64"):
 
 
 def test_native_plan_lowering_c1_is_all_apply():
+    """C1's sweep lowers to streaming passes only (APPLY, or fused SWEEP chains of APPLY steps):
+    no permute, no GEMM; every one of the 71 pairwise steps is covered by exactly one op."""
     e, p = _plan(config_task("C1"))
-    assert p.query("n_apply") == p.query("n_kernels")   # every sweep step = one APPLY pass
+    assert p.query("n_apply") + p.query("n_sweep") == p.query("n_kernels")
     assert p.query("n_permute") == 0 and p.query("n_gemm") == 0
+    assert p.query("n_apply") + p.query("n_sweep_gates") == len(e.path)
+    assert p.query("n_sweep") > 0
     assert p.n_slices == 1
 
 
@@ -86,6 +90,9 @@ def test_native_plan_c4_structure():
     gemm = [l for l in d if "GEMM" in l]
     assert "M=1024 N=1024" in gemm[0] and "[slice]" in gemm[0]
     assert p.query("n_ops_once") > 0.5 * p.query("n_kernels")   # most of the sweep is hoisted
+    # left / right sweeps are the two independent branches (two streams), the GEMM is the join
+    assert any(" b0 " in l for l in d) and any(" b1 " in l for l in d)
+    assert " b2 " in gemm[0]
     assert p.query("flops") == pytest.approx(p.query("flops_once") + 8 * p.query("flops_slice"), rel=1e-6)
 
 
