@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, f32-in MFMA
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-N_OPEN_CPU = 18                 # open outputs in the CPU-baseline sample (~10-30 s of numpy)
+N_OPEN_CPU = 20                 # open outputs in the CPU-baseline sample (one slice: ~10-30 s of numpy)
 
 
 def _pmc_traffic(config: str):
