@@ -61,6 +61,15 @@ struct GemmArgs {
 
 constexpr int kThreads = 256;
 
+// TQ_GEMM_3M=1 selects Gauss's 3-multiplication complex product in the fast path
+bool gemm_3m() {
+  static const int v = [] {
+    const char* e = getenv("TQ_GEMM_3M");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 // TQ_GEMM_FAST=0 disables the K-outer complex64 fast path (A/B timing of the two kernels)
 bool fast_disabled() {
   static const int v = [] {
@@ -316,11 +325,21 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
 //  * split-K over the grid (slab reduce kernel below); a bijective XCD remap puts all tiles of one
 //    K-split on one XCD so each XCD's L2 streams its K range of A and B from HBM exactly once.
 namespace fastc64 {
-constexpr int BM = 256, BN = 128, BK = 16, NT = 512, NSTAGE = 3;
-constexpr int A_FLOATS = BK * BM * 2, B_FLOATS = BK * BN * 2, STAGE = A_FLOATS + B_FLOATS;
-constexpr int A_PIECES_PER_WAVE = (BK * BM * 8 / 1024) / 8;  // 4
-constexpr int B_PIECES_PER_WAVE = (BK * BN * 8 / 1024) / 8;  // 2
-static_assert(A_PIECES_PER_WAVE + B_PIECES_PER_WAVE == 6, "vmcnt count below assumes 6 DMAs/tile");
+constexpr int BK = 16, NSTAGE = 3;
+// block configuration: WMW x WNW waves of 64 x 64 output each
+template <int WMW, int WNW> struct Tile {
+  static constexpr int NW = WMW * WNW, NT = 64 * NW, WMW_ = WMW;
+  static constexpr int BM = 64 * WMW, BN = 64 * WNW;
+  static constexpr int A_FLOATS = BK * BM * 2, B_FLOATS = BK * BN * 2, STAGE = A_FLOATS + B_FLOATS;
+  static constexpr int A_ROW_PIECES = BM / 128;               // 1-KiB pieces per k-row of A
+  static constexpr int A_PIECES_PER_WAVE = BK * A_ROW_PIECES / NW;
+  static constexpr int B_ROW_PIECES = BN / 128;
+  static constexpr int B_PIECES_PER_WAVE = BK * B_ROW_PIECES / NW;
+  static constexpr int NDMA = A_PIECES_PER_WAVE + B_PIECES_PER_WAVE;  // DMAs per wave per tile
+  static_assert(BK * A_ROW_PIECES % NW == 0 && BK * B_ROW_PIECES % NW == 0, "piece split");
+};
+using Tile4M = Tile<4, 2>;  // 4-multiplication complex product: 8 waves (2 per SIMD), 256 x 128
+using Tile3M = Tile<2, 2>;  // Gauss 3M: 192 accumulators need 1 wave per SIMD, 128 x 128
 }
 
 struct FastArgs {
@@ -334,12 +353,17 @@ struct FastArgs {
   float beta;
 };
 
-__global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArgs g) {
+// G3M: Gauss's 3-multiplication complex product (P1 = Ar Br, P2 = Ai Bi, P3 = (Ar+Ai)(Br+Bi);
+// Cr = P1 - P2, Ci = P3 - P1 - P2): 3 real MFMAs per complex k-step instead of 4, all in f32.
+template <bool G3M, typename TL>
+__global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) {
   using namespace fastc64;
+  constexpr int BM = TL::BM, BN = TL::BN, WMW = TL::WMW_, STAGE = TL::STAGE, A_FLOATS = TL::A_FLOATS;
+  constexpr int A_PIECES_PER_WAVE = TL::A_PIECES_PER_WAVE, B_PIECES_PER_WAVE = TL::B_PIECES_PER_WAVE;
   __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid & 3, wn = wid >> 2;
+  const int wm = wid % WMW, wn = wid / WMW;
 
   // bijective XCD remap of the linear block id, then (batch, split, tile) with tile fastest
   const int nblk = gridDim.x;
@@ -376,22 +400,28 @@ __global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArg
 #pragma unroll
     for (int q = 0; q < A_PIECES_PER_WAVE; ++q) {
       const int p = wid * A_PIECES_PER_WAVE + q;
-      glds16(A + (((int64_t)t * BK + (p >> 1)) * g.lda + (p & 1) * 128 + lane * 2) * 2, sbase + p * 256);
+      const int kr = p / TL::A_ROW_PIECES, mp = p % TL::A_ROW_PIECES;
+      glds16(A + (((int64_t)t * BK + kr) * g.lda + mp * 128 + lane * 2) * 2, sbase + p * 256);
     }
 #pragma unroll
     for (int q = 0; q < B_PIECES_PER_WAVE; ++q) {
       const int p = wid * B_PIECES_PER_WAVE + q;
-      glds16(B + (((int64_t)t * BK + p) * g.ldb + lane * 2) * 2, sbase + A_FLOATS + p * 256);
+      const int kr = p / TL::B_ROW_PIECES, np = p % TL::B_ROW_PIECES;
+      glds16(B + (((int64_t)t * BK + kr) * g.ldb + np * 128 + lane * 2) * 2, sbase + A_FLOATS + p * 256);
     }
   };
 
-  f32x16 acc_re[2][2], acc_im[2][2];
+  f32x16 acc_re[2][2], acc_im[2][2], acc_3[G3M ? 2 : 1][G3M ? 2 : 1];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { acc_re[i][j][r] = 0.f; acc_im[i][j][r] = 0.f; }
+      for (int r = 0; r < 16; ++r) {
+        acc_re[i][j][r] = 0.f;
+        acc_im[i][j][r] = 0.f;
+        if constexpr (G3M) acc_3[i][j][r] = 0.f;
+      }
 
   const int fr = lane & 31, fk = lane >> 5;
   // float offsets of this lane's fragments inside a stage (k-row kk + fk)
@@ -401,8 +431,13 @@ __global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArg
   issue(0, 0);
   if (nkt > 1) issue(1, 1);
   for (int t = 0; t < nkt; ++t) {
-    if (t + 1 < nkt) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t + 1 < nkt) {
+      if constexpr (TL::NDMA == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (TL::NDMA == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else static_assert(TL::NDMA == 6 || TL::NDMA == 8, "vmcnt");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_barrier" ::: "memory");
     if (t + 2 < nkt) issue(t + 2, (t + 2) % NSTAGE);
     const float* s = lds + (t % NSTAGE) * STAGE;
@@ -424,20 +459,34 @@ __global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArg
           nb[j] = *reinterpret_cast<const float2*>(s + b_off + ((kk + 2) * BN + j * 32) * 2);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the k+2 reads ahead of this k-step's MFMAs
+      if constexpr (G3M) {
+        float sa[2], sb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i) { sa[i] = a[i].x + a[i].y; sb[i] = bb[i].x + bb[i].y; }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc_re[i][j], 0, 0, 0);
-          acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].y, acc_im[i][j], 0, 0, 0);
-        }
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+          for (int j = 0; j < 2; ++j) {
+            acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc_re[i][j], 0, 0, 0);
+            acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].y, acc_im[i][j], 0, 0, 0);
+            acc_3[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa[i], sb[j], acc_3[i][j], 0, 0, 0);
+          }
+      } else {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(-a[i].y, bb[j].y, acc_re[i][j], 0, 0, 0);
-          acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].x, acc_im[i][j], 0, 0, 0);
-        }
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc_re[i][j], 0, 0, 0);
+            acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].y, acc_im[i][j], 0, 0, 0);
+          }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(-a[i].y, bb[j].y, acc_re[i][j], 0, 0, 0);
+            acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].x, acc_im[i][j], 0, 0, 0);
+          }
+      }
       __builtin_amdgcn_sched_barrier(0);
       if (kk + 2 < BK) {
 #pragma unroll
@@ -461,7 +510,13 @@ __global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArg
           const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int64_t gn = n0 + wn * 64 + j * 32 + (lane & 31);
           float2* p = reinterpret_cast<float2*>(Cout + (gm * ldo + gn) * 2);
-          float2 v = make_float2(acc_re[i][j][r], acc_im[i][j][r]);
+          float2 v;
+          if constexpr (G3M) {
+            const float p1 = acc_re[i][j][r], p2 = acc_im[i][j][r];
+            v = make_float2(p1 - p2, acc_3[i][j][r] - p1 - p2);
+          } else {
+            v = make_float2(acc_re[i][j][r], acc_im[i][j][r]);
+          }
           if constexpr (decltype(with_beta)::value) {
             const float2 o = *p;
             v.x += beta * o.x;
@@ -475,16 +530,21 @@ __global__ void __launch_bounds__(fastc64::NT, 1) gemm_c64_kouter_kernel(FastArg
 }
 
 // eligibility and split choice of the fast path (shared by launch and workspace sizing)
-int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
+template <typename TL>
+int fast_c64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
   using namespace fastc64;
   if (!(transA == 1 && transB == 0)) return 0;
-  if (M % BM || N % BN || K % BK || K == 0) return 0;
-  const int64_t tiles = (M / BM) * (N / BN) * batch;
+  if (M % TL::BM || N % TL::BN || K % BK || K == 0) return 0;
+  const int64_t tiles = (M / TL::BM) * (N / TL::BN) * batch;
   int s = 1;
   // fill the 256 CUs with one block each; keep >= 32 K-tiles per split
   while (tiles * s * 2 <= 256 && K % ((int64_t)s * 2 * BK) == 0 && K / ((int64_t)s * 2 * BK) >= 32) s *= 2;
   if (tiles * s > INT32_MAX) return 0;
   return s;
+}
+int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  return gemm_3m() ? fast_c64_splits_t<fastc64::Tile3M>(transA, transB, M, N, K, batch)
+                   : fast_c64_splits_t<fastc64::Tile4M>(transA, transB, M, N, K, batch);
 }
 
 // C_b = sum_s W[s][b] + beta * C_b
@@ -532,10 +592,18 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       FastArgs f{};
       f.A = (const float*)A; f.B = (const float*)B; f.C = (float*)C; f.W = (float*)W;
       f.lda = lda; f.ldb = ldb; f.ldc = ldc; f.sA = sA; f.sB = sB; f.sC = sC; f.M = M; f.N = N;
-      f.kchunk = K / fs; f.mt = (int)(M / fastc64::BM); f.nt = (int)(N / fastc64::BN);
+      const bool g3 = gemm_3m();
+      f.kchunk = K / fs;
+      f.mt = (int)(M / (g3 ? fastc64::Tile3M::BM : fastc64::Tile4M::BM));
+      f.nt = (int)(N / (g3 ? fastc64::Tile3M::BN : fastc64::Tile4M::BN));
       f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;
       const int64_t nblk = (int64_t)f.mt * f.nt * fs * batch;
-      hipLaunchKernelGGL(gemm_c64_kouter_kernel, dim3((unsigned)nblk), dim3(fastc64::NT), 0, stream, f);
+      if (g3)
+        hipLaunchKernelGGL((gemm_c64_kouter_kernel<true, fastc64::Tile3M>), dim3((unsigned)nblk),
+                           dim3(fastc64::Tile3M::NT), 0, stream, f);
+      else
+        hipLaunchKernelGGL((gemm_c64_kouter_kernel<false, fastc64::Tile4M>), dim3((unsigned)nblk),
+                           dim3(fastc64::Tile4M::NT), 0, stream, f);
       TQ_HIP(hipGetLastError());
       if (fs > 1) {
         const int64_t total = batch * M * N * 2;

@@ -1048,12 +1048,16 @@ bool graphs_disabled() {
   return v != 0;
 }
 
+void drop_graph_entry(Plan::GraphEntry& g) {
+  if (g.done) { (void)hipEventSynchronize(g.done); (void)hipEventDestroy(g.done); }
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g = Plan::GraphEntry{};
+}
+
 void drop_graph(Plan& P) {
-  if (P.graph_exec) (void)hipGraphExecDestroy(P.graph_exec);
-  if (P.graph) (void)hipGraphDestroy(P.graph);
-  P.graph_exec = nullptr;
-  P.graph = nullptr;
-  P.has_graph = false;
+  for (auto& g : P.graphs) drop_graph_entry(g);
+  P.graphs.clear();
 }
 
 }  // namespace
@@ -1091,8 +1095,16 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
   Plan::GraphKey key;
   key.inputs.assign(inputs, inputs + P.n_inputs);
   key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
-  if (!(P.has_graph && key == P.gkey)) {
-    drop_graph(P);
+  constexpr size_t kMaxGraphs = 8;
+  Plan::GraphEntry* hit = nullptr;
+  for (auto& g : P.graphs) if (g.key == key) hit = &g;
+  if (!hit) {
+    if (P.graphs.size() >= kMaxGraphs) {  // evict the least recently used (after it finished)
+      auto lru = std::min_element(P.graphs.begin(), P.graphs.end(),
+                                  [](const Plan::GraphEntry& a, const Plan::GraphEntry& b) { return a.used < b.used; });
+      drop_graph_entry(*lru);
+      P.graphs.erase(lru);
+    }
     if (!P.cap_stream) TQ_HIP(hipStreamCreateWithFlags(&P.cap_stream, hipStreamNonBlocking));
     TQ_HIP(hipStreamBeginCapture(P.cap_stream, hipStreamCaptureModeThreadLocal));
     const int rc = plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, P.cap_stream);
@@ -1103,13 +1115,18 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
       return rc;
     }
     TQ_HIP(ce);
-    P.graph = g;
-    TQ_HIP(hipGraphInstantiate(&P.graph_exec, P.graph, nullptr, nullptr, 0));
-    P.gkey = key;
-    P.has_graph = true;
+    Plan::GraphEntry e;
+    e.key = key;
+    e.graph = g;
+    TQ_HIP(hipGraphInstantiate(&e.exec, g, nullptr, nullptr, 0));
+    TQ_HIP(hipEventCreateWithFlags(&e.done, hipEventDisableTiming));
+    P.graphs.push_back(e);
+    hit = &P.graphs.back();
     ++P.graph_builds;
   }
-  TQ_HIP(hipGraphLaunch(P.graph_exec, stream));
+  hit->used = ++P.graph_clock;
+  TQ_HIP(hipGraphLaunch(hit->exec, stream));
+  TQ_HIP(hipEventRecord(hit->done, stream));
   ++P.graph_launches;
   return TQ_OK;
 }

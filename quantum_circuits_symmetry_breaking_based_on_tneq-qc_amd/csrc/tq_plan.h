@@ -117,10 +117,17 @@ struct Plan {
     }
   };
   bool use_graph = true;
-  bool has_graph = false;
-  GraphKey gkey;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t graph_exec = nullptr;
+  // small cache of instantiated graphs (alternating slice ranges / buffers do not re-capture);
+  // an entry is destroyed only after the event recorded behind its last launch has completed
+  struct GraphEntry {
+    GraphKey key;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t used = 0;
+  };
+  std::vector<GraphEntry> graphs;
+  uint64_t graph_clock = 0;
   hipStream_t cap_stream = nullptr;
   hipStream_t side_stream = nullptr;        // branch-1 ops
   std::vector<hipEvent_t> sync_events;      // fork / join events (reused)
