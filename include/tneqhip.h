@@ -55,6 +55,11 @@ enum {
 int tq_version(void);                      /* (major << 16) | minor */
 int tq_last_error(char* buf, size_t n);    /* copies the last error of this thread; returns its length */
 int tq_device_synchronize(void);
+/* Library configuration: "gemm_3m" (1: complex64 fast GEMM uses Gauss's 3-multiplication
+ * product, env TQ_GEMM_3M=0 turns it off), "sweep" (fused multi-gate sweeps, env TQ_SWEEP),
+ * "graphs" (plan execution through hipGraphs, env TQ_GRAPH).  -1 if unknown.  No reference
+ * counterpart (the reference has no native layer); used for measurement reports. */
+int64_t tq_library_query(const char* key);
 
 /* ---- kernels ----------------------------------------------------------------------- */
 

@@ -14,6 +14,21 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 const std::string& last_error() { return g_last_error; }
 }  // namespace tq
 
+namespace tq {
+bool gemm_3m();
+bool graphs_enabled();
+bool sweeps_enabled_global();
+}
+
+extern "C" int64_t tq_library_query(const char* key) {
+  if (!key) return -1;
+  const std::string k(key);
+  if (k == "gemm_3m") return tq::gemm_3m() ? 1 : 0;
+  if (k == "graphs") return tq::graphs_enabled() ? 1 : 0;
+  if (k == "sweep") return tq::sweeps_enabled_global() ? 1 : 0;
+  return -1;
+}
+
 struct tq_plan_s {
   tq::Plan plan;
   bool materialized = false;

@@ -21,6 +21,18 @@
 
 namespace tq {
 
+// The fast path computes complex products with Gauss's 3 real multiplications (default; the C4
+// amplitudes stay within 4.0e-6 of complex128, vs 2.7e-6 for the 4-multiplication product);
+// TQ_GEMM_3M=0 selects the 4-multiplication kernel.
+bool gemm_3m() {
+  static const int v = [] {
+    const char* e = getenv("TQ_GEMM_3M");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v != 0;
+}
+
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -60,15 +72,6 @@ struct GemmArgs {
 };
 
 constexpr int kThreads = 256;
-
-// TQ_GEMM_3M=1 selects Gauss's 3-multiplication complex product in the fast path
-bool gemm_3m() {
-  static const int v = [] {
-    const char* e = getenv("TQ_GEMM_3M");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return v != 0;
-}
 
 // TQ_GEMM_FAST=0 disables the K-outer complex64 fast path (A/B timing of the two kernels)
 bool fast_disabled() {
@@ -326,10 +329,12 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
 //    K-split on one XCD so each XCD's L2 streams its K range of A and B from HBM exactly once.
 namespace fastc64 {
 constexpr int BK = 16, NSTAGE = 3;
-// block configuration: WMW x WNW waves of 64 x 64 output each
-template <int WMW, int WNW> struct Tile {
-  static constexpr int NW = WMW * WNW, NT = 64 * NW, WMW_ = WMW;
-  static constexpr int BM = 64 * WMW, BN = 64 * WNW;
+// block configuration: WMW x WNW waves, each owning TI x TJ tiles of 32 x 32 outputs
+template <int WMW_, int WNW_, int TI_, int TJ_> struct Tile {
+  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_;
+  static constexpr int NW = WMW * WNW, NT = 64 * NW;
+  static constexpr int WM = 32 * TI, WN = 32 * TJ;            // wave tile
+  static constexpr int BM = WMW * WM, BN = WNW * WN;           // block tile
   static constexpr int A_FLOATS = BK * BM * 2, B_FLOATS = BK * BN * 2, STAGE = A_FLOATS + B_FLOATS;
   static constexpr int A_ROW_PIECES = BM / 128;               // 1-KiB pieces per k-row of A
   static constexpr int A_PIECES_PER_WAVE = BK * A_ROW_PIECES / NW;
@@ -338,8 +343,11 @@ template <int WMW, int WNW> struct Tile {
   static constexpr int NDMA = A_PIECES_PER_WAVE + B_PIECES_PER_WAVE;  // DMAs per wave per tile
   static_assert(BK * A_ROW_PIECES % NW == 0 && BK * B_ROW_PIECES % NW == 0, "piece split");
 };
-using Tile4M = Tile<4, 2>;  // 4-multiplication complex product: 8 waves (2 per SIMD), 256 x 128
-using Tile3M = Tile<2, 2>;  // Gauss 3M: 192 accumulators need 1 wave per SIMD, 128 x 128
+// 4-multiplication complex product: 8 waves (2 per SIMD) of 64 x 64, block 256 x 128
+using Tile4M = Tile<4, 2, 2, 2>;
+// Gauss 3M (3 accumulator sets): 8 waves of 64 x 32 keep 96 accumulators (2 waves per SIMD),
+// block 128 x 128
+using Tile3M = Tile<2, 4, 2, 1>;
 }
 
 struct FastArgs {
@@ -358,8 +366,10 @@ struct FastArgs {
 template <bool G3M, typename TL>
 __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) {
   using namespace fastc64;
-  constexpr int BM = TL::BM, BN = TL::BN, WMW = TL::WMW_, STAGE = TL::STAGE, A_FLOATS = TL::A_FLOATS;
+  constexpr int BM = TL::BM, BN = TL::BN, WMW = TL::WMW, TI = TL::TI, TJ = TL::TJ;
+  constexpr int STAGE = TL::STAGE, A_FLOATS = TL::A_FLOATS;
   constexpr int A_PIECES_PER_WAVE = TL::A_PIECES_PER_WAVE, B_PIECES_PER_WAVE = TL::B_PIECES_PER_WAVE;
+  constexpr int NACC = G3M ? 3 : 2;
   __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -384,10 +394,10 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
   const float* A = g.A + ((int64_t)b * g.sA + kbeg * g.lda + m0) * 2;
   const float* B = g.B + ((int64_t)b * g.sB + kbeg * g.ldb + n0) * 2;
 
-  // this wave's DMA pieces: A piece p (0..31) = k-row p/2, m-half p%2; B piece p (0..15) = k-row p.
-  // The DMA is issued from inline asm: hipcc would otherwise treat every in-flight LDS-DMA as a
-  // possible alias of the next ds_read and drain it with vmcnt(0) (cdna_hip_programming.md §5
-  // trap 4(a)); the counted waits below are the only ordering, placed by hand.
+  // this wave's DMA pieces (1 KiB = 128 complex of one k-row each).  The DMA is issued from
+  // inline asm: hipcc would otherwise treat every in-flight LDS-DMA as a possible alias of the
+  // next ds_read and drain it with vmcnt(0) (cdna_hip_programming.md §5 trap 4(a)); the counted
+  // waits below are the only ordering, placed by hand.
   const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)lds;
   auto glds16 = [&](const float* gsrc, unsigned lds_off_floats) {
     unsigned keep;
@@ -411,86 +421,89 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
     }
   };
 
-  f32x16 acc_re[2][2], acc_im[2][2], acc_3[G3M ? 2 : 1][G3M ? 2 : 1];
+  f32x16 acc[NACC][TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int x = 0; x < NACC; ++x)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc_re[i][j][r] = 0.f;
-        acc_im[i][j][r] = 0.f;
-        if constexpr (G3M) acc_3[i][j][r] = 0.f;
-      }
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][i][j][r] = 0.f;
 
   const int fr = lane & 31, fk = lane >> 5;
   // float offsets of this lane's fragments inside a stage (k-row kk + fk)
-  const int a_off = (fk * BM + wm * 64 + fr) * 2;
-  const int b_off = A_FLOATS + (fk * BN + wn * 64 + fr) * 2;
+  const int a_off = (fk * BM + wm * TL::WM + fr) * 2;
+  const int b_off = A_FLOATS + (fk * BN + wn * TL::WN + fr) * 2;
 
   issue(0, 0);
   if (nkt > 1) issue(1, 1);
   for (int t = 0; t < nkt; ++t) {
     if (t + 1 < nkt) {
       if constexpr (TL::NDMA == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (TL::NDMA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else if constexpr (TL::NDMA == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else static_assert(TL::NDMA == 6 || TL::NDMA == 8, "vmcnt");
+      else static_assert(TL::NDMA == 4 || TL::NDMA == 6 || TL::NDMA == 8, "vmcnt");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("s_barrier" ::: "memory");
     if (t + 2 < nkt) issue(t + 2, (t + 2) % NSTAGE);
     const float* s = lds + (t % NSTAGE) * STAGE;
-    // fragments of k-step kk+2 are read while the 16 MFMAs of k-step kk run
-    float2 a[2], bb[2];
+    // fragments of k-step kk+2 are read while the MFMAs of k-step kk run
+    float2 a[TI], bb[TJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const float2*>(s + a_off + (i * 32) * 2);
+    for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const float2*>(s + a_off + (i * 32) * 2);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bb[j] = *reinterpret_cast<const float2*>(s + b_off + (j * 32) * 2);
+    for (int j = 0; j < TJ; ++j) bb[j] = *reinterpret_cast<const float2*>(s + b_off + (j * 32) * 2);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      float2 na[2], nb[2];
+      float2 na[TI], nb[TJ];
       if (kk + 2 < BK) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
           na[i] = *reinterpret_cast<const float2*>(s + a_off + ((kk + 2) * BM + i * 32) * 2);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TJ; ++j)
           nb[j] = *reinterpret_cast<const float2*>(s + b_off + ((kk + 2) * BN + j * 32) * 2);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the k+2 reads ahead of this k-step's MFMAs
       if constexpr (G3M) {
-        float sa[2], sb[2];
+        float sa[TI], sb[TJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) { sa[i] = a[i].x + a[i].y; sb[i] = bb[i].x + bb[i].y; }
+        for (int i = 0; i < TI; ++i) sa[i] = a[i].x + a[i].y;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < TJ; ++j) sb[j] = bb[j].x + bb[j].y;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc_re[i][j], 0, 0, 0);
-            acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].y, acc_im[i][j], 0, 0, 0);
-            acc_3[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa[i], sb[j], acc_3[i][j], 0, 0, 0);
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc[0][i][j], 0, 0, 0);
+            acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].y, acc[1][i][j], 0, 0, 0);
+            acc[NACC - 1][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa[i], sb[j], acc[NACC - 1][i][j], 0, 0, 0);
           }
       } else {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc_re[i][j], 0, 0, 0);
-            acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].y, acc_im[i][j], 0, 0, 0);
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].x, acc[0][i][j], 0, 0, 0);
+            acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, bb[j].y, acc[1][i][j], 0, 0, 0);
           }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc_re[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(-a[i].y, bb[j].y, acc_re[i][j], 0, 0, 0);
-            acc_im[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].x, acc_im[i][j], 0, 0, 0);
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(-a[i].y, bb[j].y, acc[0][i][j], 0, 0, 0);
+            acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, bb[j].x, acc[1][i][j], 0, 0, 0);
           }
       }
       __builtin_amdgcn_sched_barrier(0);
       if (kk + 2 < BK) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) { a[i] = na[i]; bb[i] = nb[i]; }
+        for (int i = 0; i < TI; ++i) a[i] = na[i];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bb[j] = nb[j];
       }
     }
   }
@@ -502,20 +515,20 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
   const float beta = partial ? 0.f : g.beta;
   auto store = [&](auto with_beta) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int64_t gn = n0 + wn * 64 + j * 32 + (lane & 31);
+          const int64_t gm = m0 + wm * TL::WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int64_t gn = n0 + wn * TL::WN + j * 32 + (lane & 31);
           float2* p = reinterpret_cast<float2*>(Cout + (gm * ldo + gn) * 2);
           float2 v;
           if constexpr (G3M) {
-            const float p1 = acc_re[i][j][r], p2 = acc_im[i][j][r];
-            v = make_float2(p1 - p2, acc_3[i][j][r] - p1 - p2);
+            const float p1 = acc[0][i][j][r], p2 = acc[1][i][j][r];
+            v = make_float2(p1 - p2, acc[NACC - 1][i][j][r] - p1 - p2);
           } else {
-            v = make_float2(acc_re[i][j][r], acc_im[i][j][r]);
+            v = make_float2(acc[0][i][j][r], acc[1][i][j][r]);
           }
           if constexpr (decltype(with_beta)::value) {
             const float2 o = *p;

@@ -1038,6 +1038,11 @@ int plan_profile_read(Plan& P, int kind, double* ms, int64_t* launches, double* 
   return TQ_OK;
 }
 
+bool sweeps_enabled_global() {
+  const char* e = getenv("TQ_SWEEP");
+  return !(e && e[0] == '0');
+}
+
 namespace {
 
 bool graphs_disabled() {
@@ -1047,6 +1052,10 @@ bool graphs_disabled() {
   }();
   return v != 0;
 }
+
+}  // namespace
+bool graphs_enabled() { return !graphs_disabled(); }
+namespace {
 
 void drop_graph_entry(Plan::GraphEntry& g) {
   if (g.done) { (void)hipEventSynchronize(g.done); (void)hipEventDestroy(g.done); }
