@@ -184,6 +184,9 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "n_permute") return P.n_permute;
   if (k == "n_sweep") return P.n_sweep;
   if (k == "n_sweep_gates") return P.n_sweep_gates;
+  if (k == "n_sweep2") { int64_t c = 0; for (auto& o : P.ops) c += o.kind == tq::OP_SWEEP2; return c; }
+  if (k == "n_launch_once") return P.n_launch_once;
+  if (k == "n_launch_slice") return P.n_launch_slice;
   if (k == "out_numel") return P.out_numel;
   return -1;
 }

@@ -263,17 +263,94 @@ class Compiler {
       P_.n_gemm += op.kind == OP_GEMM;
       P_.n_apply += op.kind == OP_APPLY;
       P_.n_permute += op.kind == OP_PERMUTE;
-      P_.n_sweep += op.kind == OP_SWEEP;
-      if (op.kind == OP_SWEEP) P_.n_sweep_gates += (int)op.sgates.size();
+      P_.n_sweep += op.kind == OP_SWEEP || op.kind == OP_SWEEP2;
+      if (op.kind == OP_SWEEP || op.kind == OP_SWEEP2) P_.n_sweep_gates += (int)op.sgates.size();
     }
+    build_schedule();
     P_.flops = P_.flops_once + P_.flops_slice * (double)P_.n_slices;
     P_.bytes = P_.bytes_once + P_.bytes_slice * (double)P_.n_slices;
     std::ostringstream d;
     for (size_t i = 0; i < P_.ops.size(); ++i)
       d << (P_.ops[i].invariant ? "[once]  " : "[slice] ") << "b" << P_.ops[i].branch << " "
         << P_.ops[i].note << "\n";
+    d << "# schedule (launch: op indices)\n";
+    for (int set = 0; set < 2; ++set)
+      for (auto& g : set == 0 ? P_.sched_once : P_.sched_slice) {
+        d << "# " << (set == 0 ? "once " : "slice");
+        for (int j : g) d << " " << j;
+        d << "\n";
+      }
     P_.describe = d.str();
     return TQ_OK;
+  }
+
+  // Launch schedule.  Ops of one set (slice-invariant / per slice) are ordered by dependency
+  // level: an op's level is one more than that of every earlier op it conflicts with (RAW, WAR
+  // or WAW on overlapping bytes of the arena, the output or a workspace; inputs are read-only).
+  // Ops of one level commute, so the independent in-place sweeps of a level (e.g. the left and
+  // right subtrees of a cut network, or the tiny vector pre-absorption chains) share a launch.
+  void build_schedule() {
+    struct Acc { int space; int64_t lo, hi; };
+    const int64_t esz = (int64_t)P_.esz;
+    auto add = [&](std::vector<Acc>& v, const BufRef& b, int64_t n) {
+      if (n <= 0) return;
+      switch (b.kind) {
+        case BUF_ARENA: v.push_back({0, b.off * esz, (b.off + n) * esz}); break;
+        case BUF_PINNED:
+          v.push_back({0, (int64_t)P_.pinned_base + b.off * esz, (int64_t)P_.pinned_base + (b.off + n) * esz});
+          break;
+        case BUF_OUTPUT: v.push_back({1, b.off * esz, (b.off + n) * esz}); break;
+        default: break;  // inputs are never written
+      }
+    };
+    const size_t n = P_.ops.size();
+    std::vector<std::vector<Acc>> rd(n), wr(n);
+    for (size_t i = 0; i < n; ++i) {
+      const Op& op = P_.ops[i];
+      add(rd[i], op.a, op.na);
+      add(rd[i], op.b, op.nb);
+      add(wr[i], op.c, op.nc);
+      add(rd[i], op.c, op.nc);    // beta accumulation reads the target
+      add(wr[i], op.ws, op.nws);
+      add(rd[i], op.ws, op.nws);
+      for (auto& g : op.sgates) add(rd[i], g.g, g.n);
+    }
+    auto overlap = [](const std::vector<Acc>& x, const std::vector<Acc>& y) {
+      for (auto& a : x)
+        for (auto& b : y)
+          if (a.space == b.space && a.lo < b.hi && b.lo < a.hi) return true;
+      return false;
+    };
+    for (int set = 0; set < 2; ++set) {
+      std::vector<int> ids;
+      for (size_t i = 0; i < n; ++i) if (P_.ops[i].invariant == (set == 0)) ids.push_back((int)i);
+      std::vector<int> lev(ids.size(), 0);
+      int maxlev = -1;
+      for (size_t b = 0; b < ids.size(); ++b) {
+        const int j = ids[b];
+        for (size_t a = 0; a < b; ++a) {
+          const int i = ids[a];
+          if (lev[a] + 1 <= lev[b]) continue;
+          if (overlap(wr[i], rd[j]) || overlap(wr[i], wr[j]) || overlap(rd[i], wr[j])) lev[b] = lev[a] + 1;
+        }
+        maxlev = std::max(maxlev, lev[b]);
+      }
+      auto& sched = set == 0 ? P_.sched_once : P_.sched_slice;
+      sched.clear();
+      for (int L = 0; L <= maxlev; ++L) {
+        std::vector<int> grp;
+        for (size_t b = 0; b < ids.size(); ++b) {
+          if (lev[b] != L) continue;
+          const int j = ids[b];
+          if (P_.ops[j].kind != OP_SWEEP2) { sched.push_back({j}); continue; }
+          grp.push_back(j);
+          if ((int)grp.size() == kS2MaxOps) { sched.push_back(grp); grp.clear(); }
+        }
+        if (!grp.empty()) sched.push_back(grp);
+      }
+    }
+    P_.n_launch_once = (int)P_.sched_once.size();
+    P_.n_launch_slice = (int)P_.sched_slice.size();
   }
 
  private:
@@ -335,6 +412,8 @@ class Compiler {
     op.perm = (int)P_.perms.size();
     op.step = step;
     const int64_t n = prod(shape);
+    op.na = X.numel();
+    op.nc = n;
     op.bytes = 2.0 * n * P_.esz;
     std::ostringstream o;
     o << "step " << step << " PERMUTE " << why << " " << modes_str(X.modes) << "->" << modes_str(order)
@@ -558,6 +637,9 @@ class Compiler {
     op.c = tgt;
     op.writes_output = direct;
     op.O = d.O; op.K = d.K1; op.M = d.M; op.K2 = d.K2; op.N = d.N; op.I = d.I;
+    op.na = d.O * d.K1 * d.M * d.K2 * d.I;
+    op.nb = Sm.numel();
+    op.nc = outn;
     op.step = s;
     op.flops = (double)d.O * d.M * d.I * d.K * d.N * (cplx_ ? 8.0 : 2.0);
     op.bytes = (double)(d.O * d.K * d.M * d.I + outn + d.K * d.N) * P_.esz;
@@ -596,6 +678,7 @@ class Compiler {
     std::vector<int> out_modes;
   };
   struct ChainShape {
+    bool s2 = false;      // fits the in-place butterfly sweep (tq_sweep2.hip)
     std::vector<int> tin, tout, outer;
     std::vector<std::vector<int>> W;   // working-set mode lists after each gate (W[q-1] = tout)
     int64_t tin_n = 1, tout_n = 1, wmax = 1;
@@ -656,7 +739,263 @@ class Compiler {
     sh.wmax = std::max({sh.wmax, sh.tin_n, sh.tout_n});
     int64_t tab = 0;
     for (size_t j = 0; j < c.gates.size(); ++j) tab += count_of(sh.W[j]) * (c.gates[j].d.K + 1);
-    return sh.wmax <= sweep_wmax((int)P_.esz) && tab <= kSweepTabMax;
+    const bool old_ok = sh.wmax <= sweep_wmax((int)P_.esz) && tab <= kSweepTabMax;
+    sh.s2 = s2_layout(c, sh, out_modes, nullptr);
+    return old_ok || sh.s2;
+  }
+
+  static int ilog2(int64_t v) {
+    if (v <= 0 || (v & (v - 1))) return -1;
+    int l = 0;
+    while ((int64_t(1) << l) < v) ++l;
+    return l;
+  }
+  static int s2_min_chunks() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_MINCHUNKS");
+      return e ? atoi(e) : 256;
+    }();
+    return v;
+  }
+  static bool s2_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_SWEEP2");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
+  // GF(2) rank of a few small bit vectors
+  static int gf2_rank(std::vector<int> v) {
+    int r = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+      int piv = -1;
+      for (size_t i = r; i < v.size(); ++i) if ((v[i] >> bit) & 1) { piv = (int)i; break; }
+      if (piv < 0) continue;
+      std::swap(v[r], v[piv]);
+      for (size_t i = 0; i < v.size(); ++i) if ((int)i != r && ((v[i] >> bit) & 1)) v[i] ^= v[r];
+      ++r;
+    }
+    return r;
+  }
+
+  // Layout of an in-place butterfly sweep (tq_sweep2.hip): every mode bit of the working set
+  // gets a tile position (input tile bits memory-fastest first; a gate's outputs reuse the
+  // positions it frees), the columns are the untouched mode bits ordered by stride, and a
+  // per-position XOR swizzle keeps the half-wave LDS accesses of the load / store phases
+  // conflict-free.  False if the chain does not fit (non power-of-two extents, K or N > 8,
+  // more than s2_max_pos live bits).
+  bool s2_layout(const Chain& c, const ChainShape& sh, const std::vector<int>& out_modes,
+                 S2Desc* out) {
+    if (!s2_enabled() || c.gates.empty() || (int)c.gates.size() > kS2MaxGates) return false;
+    const int maxpos = s2_max_pos((int)P_.esz);
+    auto nbits = [&](int m) { return ilog2(ext_[m]); };
+    for (int m : c.X0.modes) if (nbits(m) < 0) return false;
+    if (!c.X0.contiguous()) return false;
+    for (auto& g : c.gates) {
+      if (g.d.K > kS2MaxK || g.d.N > kS2MaxKN) return false;
+      for (int m : g.d.nfree) if (nbits(m) < 0) return false;
+    }
+    std::map<int, int64_t> sx, sy;
+    {
+      auto cs = contig_strides(c.X0.ext);
+      for (size_t q = 0; q < c.X0.modes.size(); ++q) sx[c.X0.modes[q]] = cs[q];
+      std::vector<int64_t> ye;
+      for (int m : out_modes) ye.push_back(ext_[m]);
+      auto cy = contig_strides(ye);
+      for (size_t q = 0; q < out_modes.size(); ++q) sy[out_modes[q]] = cy[q];
+    }
+    typedef std::pair<int, int> MB;  // (mode, bit of its index)
+    std::map<MB, int> pos;
+    std::vector<std::pair<int64_t, MB>> tb;
+    for (int m : sh.tin) for (int i = 0; i < nbits(m); ++i) tb.push_back({sx[m] << i, {m, i}});
+    std::sort(tb.begin(), tb.end());
+    uint32_t live = 0;
+    int used = 0;
+    for (auto& t : tb) {
+      if (used >= maxpos) return false;
+      pos[t.second] = used;
+      live |= 1u << used;
+      ++used;
+    }
+    const std::map<MB, int> pos_in = pos;
+    S2Desc d;
+    d.ngates = (int)c.gates.size();
+    std::vector<std::vector<int>> kdep(c.gates.size()), ndep(c.gates.size());
+    for (size_t j = 0; j < c.gates.size(); ++j) {
+      const auto& g = c.gates[j];
+      std::vector<MB> kb, nb;   // index bits, least significant first
+      for (auto it = g.d.korder.rbegin(); it != g.d.korder.rend(); ++it)
+        for (int i = 0; i < nbits(*it); ++i) kb.push_back({*it, i});
+      for (auto it = g.d.nfree.rbegin(); it != g.d.nfree.rend(); ++it)
+        for (int i = 0; i < nbits(*it); ++i) nb.push_back({*it, i});
+      if ((int64_t(1) << kb.size()) != g.d.K || (int64_t(1) << nb.size()) != g.d.N) return false;
+      uint32_t kmask = 0;
+      std::vector<int> freed, kp;
+      for (auto& b : kb) {
+        auto f = pos.find(b);
+        if (f == pos.end()) return false;
+        kmask |= 1u << f->second;
+        freed.push_back(f->second);
+        kp.push_back(f->second);
+        pos.erase(f);
+      }
+      S2Gate& G = d.gate[j];
+      G.K = (int)g.d.K;
+      G.N = (int)g.d.N;
+      G.pass_mask = live & ~kmask;
+      live &= ~kmask;
+      std::vector<int> np;
+      size_t fi = 0;
+      for (auto& b : nb) {
+        int p;
+        if (fi < freed.size()) p = freed[fi++];
+        else {
+          p = 0;
+          while (p < maxpos && ((live >> p) & 1)) ++p;
+          if (p >= maxpos) return false;
+        }
+        pos[b] = p;
+        live |= 1u << p;
+        np.push_back(p);
+        used = std::max(used, p + 1);
+      }
+      for (int k = 0; k < G.K; ++k) {
+        int v = 0;
+        for (size_t t = 0; t < kp.size(); ++t) if ((k >> t) & 1) v |= 1 << kp[t];
+        kdep[j].push_back(v);
+      }
+      for (int n = 0; n < G.N; ++n) {
+        int v = 0;
+        for (size_t t = 0; t < np.size(); ++t) if ((n >> t) & 1) v |= 1 << np[t];
+        ndep[j].push_back(v);
+      }
+      for (int t = 0; t < G.K * G.N; ++t) G.gidx[t] = g.d.gtab.empty() ? t : g.d.gtab[t];
+    }
+    // the final working set must be the output tile
+    {
+      std::set<MB> want;
+      for (int m : sh.tout) for (int i = 0; i < nbits(m); ++i) want.insert({m, i});
+      std::set<MB> have;
+      for (auto& kv : pos) have.insert(kv.first);
+      if (want != have) return false;
+    }
+    if (!out) return true;
+    // columns: untouched mode bits by increasing stride
+    std::vector<std::pair<int64_t, int64_t>> cb;  // (stride in X, stride in Y)
+    for (int m : sh.outer) for (int i = 0; i < nbits(m); ++i) cb.push_back({sx[m] << i, sy.at(m) << i});
+    std::sort(cb.begin(), cb.end());
+    if ((int)cb.size() > kS2MaxColBits) return false;
+    d.colbits = (int)cb.size();
+    d.ncols = int64_t(1) << d.colbits;
+    for (size_t j = 0; j < cb.size(); ++j) { d.w_in[j] = cb[j].first; d.w_out[j] = cb[j].second; }
+    const int lc_cap = s2_chunk_bits((int)P_.esz) - used;
+    if (lc_cap < 0) return false;
+    int lc = std::max(5, d.colbits - 10);
+    lc = std::min(lc, lc_cap);
+    lc = std::min(lc, d.colbits);
+    // small tensors: narrower chunks, so that the op still spreads over >= s2_min_chunks()
+    // workgroups (a 2^19-element tensor with a 256-element tile has only 64 chunks of 32 columns)
+    if (const int mc = s2_min_chunks(); mc > 1) {
+      int lg = 0;
+      while ((2 << lg) <= mc) ++lg;
+      lc = std::min(lc, std::max(std::min(2, d.colbits), d.colbits - lg));
+    }
+    d.logC = lc;
+    d.nchunks = int64_t(1) << (d.colbits - lc);
+    // load / store enumerations: chunk bits by increasing memory stride
+    struct CBit { int64_t w; int col; int pos; };  // col >= 0: column bit, else tile position
+    std::vector<CBit> ld, st;
+    for (int j = 0; j < lc; ++j) { ld.push_back({cb[j].first, j, -1}); st.push_back({cb[j].second, j, -1}); }
+    for (auto& kv : pos_in) ld.push_back({sx[kv.first.first] << kv.first.second, -1, kv.second});
+    for (auto& kv : pos) st.push_back({sy.at(kv.first.first) << kv.first.second, -1, kv.second});
+    auto by_w = [](const CBit& a, const CBit& b) { return a.w < b.w; };
+    std::sort(ld.begin(), ld.end(), by_w);
+    std::sort(st.begin(), st.end(), by_w);
+    // swizzle vectors: the first 4 / 5 chunk bits of each enumeration (one 16- / 32-lane group)
+    // must map to independent bank slots (mod 16 / mod 32)
+    int vsw[8];
+    for (int& v : vsw) v = -1;
+    auto choose = [&](const std::vector<CBit>& e) {
+      std::vector<int> vec;
+      for (size_t t = 0; t < e.size() && t < 5; ++t) {
+        if (e[t].col >= 0) { vec.push_back(e[t].col < 5 ? (1 << e[t].col) : 0); continue; }
+        int& v = vsw[e[t].pos];
+        if (v < 0) {
+          static const int order[] = {1, 2, 4, 8, 16, 3, 5, 6, 9, 10, 12, 17, 18, 20, 24, 7, 11, 13,
+                                      14, 19, 21, 22, 25, 26, 28, 15, 23, 27, 29, 30, 31};
+          v = 0;
+          for (int cand : order) {
+            std::vector<int> a = vec, b;
+            a.push_back(cand);
+            for (size_t q = 0; q < a.size() && q < 4; ++q) b.push_back(a[q] & 15);
+            if (gf2_rank(a) == (int)a.size() && gf2_rank(b) == (int)b.size()) { v = cand; break; }
+          }
+        }
+        vec.push_back(v);
+      }
+    };
+    choose(ld);
+    choose(st);
+    for (int p = 0; p < 8; ++p) d.vsw[p] = vsw[p] < 0 ? 0 : vsw[p];
+    auto code = [&](const CBit& b) {
+      if (b.col >= 0) return 1 << b.col;
+      return ((1 << b.pos) << kS2CodeP) | (d.vsw[b.pos] << kS2CodeS);
+    };
+    d.nld = (int)ld.size();
+    d.nst = (int)st.size();
+    if (d.nld > 16 || d.nst > 16) return false;
+    for (size_t t = 0; t < ld.size(); ++t) { d.ld_w[t] = ld[t].w; d.ld_code[t] = code(ld[t]); }
+    for (size_t t = 0; t < st.size(); ++t) { d.st_w[t] = st[t].w; d.st_code[t] = code(st[t]); }
+    // LDS element address of a code: (p << logC) + (c ^ (s & (C-1))) -- XOR-linear in the code
+    auto lds_addr = [&](int cd) {
+      const int p = (cd >> kS2CodeP) & 0xFF, cc = cd & ((1 << kS2CodeP) - 1), sv = (cd >> kS2CodeS) & 31;
+      return (p << d.logC) + (cc ^ (sv & ((1 << d.logC) - 1)));
+    };
+    for (int t = 0; t < d.nld; ++t) d.ld_a[t] = lds_addr(d.ld_code[t]);
+    for (int t = 0; t < d.nst; ++t) d.st_a[t] = lds_addr(d.st_code[t]);
+    const int rin = std::max(1, (1 << d.nld) >> kS2LogThreads), rout = std::max(1, (1 << d.nst) >> kS2LogThreads);
+    for (int r = 0; r < kS2MaxSlots; ++r) {
+      const int ri = r % rin, ro = r % rout;
+      for (int b = kS2LogThreads; b < d.nld; ++b)
+        if ((ri >> (b - kS2LogThreads)) & 1) { d.ld_hm[r] += d.ld_w[b]; d.ld_hc[r] ^= d.ld_code[b]; }
+      for (int b = kS2LogThreads; b < d.nst; ++b)
+        if ((ro >> (b - kS2LogThreads)) & 1) { d.st_hm[r] += d.st_w[b]; d.st_hc[r] ^= d.st_code[b]; }
+      d.ld_ha[r] = lds_addr(d.ld_hc[r]);
+      d.st_ha[r] = lds_addr(d.st_hc[r]);
+    }
+    auto swz = [&](int bits) {
+      int v = 0;
+      for (int p = 0; p < 8; ++p) if ((bits >> p) & 1) v ^= d.vsw[p];
+      return v;
+    };
+    const int cmask = (1 << d.logC) - 1;
+    for (size_t j = 0; j < c.gates.size(); ++j) {
+      S2Gate& G = d.gate[j];
+      for (int k = 0; k < G.K; ++k) {
+        G.kdep[k] = kdep[j][k];
+        G.ksw[k] = swz(kdep[j][k]);
+        G.kaddr[k] = (G.kdep[k] << d.logC) ^ (G.ksw[k] & cmask);
+      }
+      for (int n = 0; n < G.N; ++n) {
+        G.ndep[n] = ndep[j][n];
+        G.nsw[n] = swz(ndep[j][n]);
+        G.naddr[n] = (G.ndep[n] << d.logC) ^ (G.nsw[n] & cmask);
+      }
+    }
+    if (getenv("TQ_DEBUG_S2")) {
+      fprintf(stderr, "S2 cols=2^%d logC=%d used=%d ld:", d.colbits, d.logC, used);
+      for (int t = 0; t < d.nld; ++t) fprintf(stderr, " %lld/%x", (long long)d.ld_w[t], d.ld_code[t]);
+      fprintf(stderr, " | st:");
+      for (int t = 0; t < d.nst; ++t) fprintf(stderr, " %lld/%x", (long long)d.st_w[t], d.st_code[t]);
+      fprintf(stderr, " | vsw:");
+      for (int p = 0; p < 8; ++p) fprintf(stderr, " %d", d.vsw[p]);
+      fprintf(stderr, " | gates:");
+      for (size_t j = 0; j < c.gates.size(); ++j)
+        fprintf(stderr, " [K%d N%d pass%x]", d.gate[j].K, d.gate[j].N, d.gate[j].pass_mask);
+      fprintf(stderr, "\n");
+    }
+    *out = d;
+    return true;
   }
 
   // mixed-radix digits of index t over `modes` (last fastest)
@@ -684,14 +1023,65 @@ class Compiler {
     const int saved_br = br_;
     pin_next_ = pinned_[c.id];
     br_ = c.br;
-    if (c.gates.size() == 1) {
+    ChainShape sh0;
+    const bool shape_ok = chain_shape(c, c.out_modes, sh0);
+    if (c.gates.size() == 1 && !(shape_ok && sh0.s2)) {
       const auto& g = c.gates[0];
       const Live& A0 = g.d.a_big ? c.X0 : g.Sm;
       const Live& B0 = g.d.a_big ? g.Sm : c.X0;
       TQ_TRY(emit_apply(g.step, g.d, final, A0, B0, res));
+    } else if (shape_ok && sh0.s2) {
+      S2Desc d;
+      if (!s2_layout(c, sh0, c.out_modes, &d)) { set_error("internal: sweep2 layout"); return TQ_ERR_INVALID; }
+      const int64_t n0 = c.X0.numel();
+      const int64_t nq = n0 / sh0.tin_n * sh0.tout_n;
+      bool direct;
+      int64_t roff;
+      BufRef tgt = result_target(final, c.out_modes, nq, &direct, &roff);
+      Op op;
+      op.kind = OP_SWEEP2;
+      op.a = c.X0.buf;
+      op.c = tgt;
+      op.writes_output = direct;
+      op.step = c.gates.back().step;
+      op.tin = (int)sh0.tin_n;
+      op.tout = (int)sh0.tout_n;
+      op.ncols = d.ncols;
+      op.s2_nchunks = d.nchunks;
+      op.na = n0;
+      op.nc = nq;
+      double flops = 0;
+      for (size_t j = 0; j < c.gates.size(); ++j) {
+        SweepGate sg;
+        sg.g = c.gates[j].Sm.buf;
+        sg.K = (int)c.gates[j].d.K;
+        sg.N = (int)c.gates[j].d.N;
+        sg.n = c.gates[j].Sm.numel();
+        op.sgates.push_back(sg);
+        flops += (double)d.ncols * count_of(sh0.W[j]) * sg.K * (cplx_ ? 8.0 : 2.0);
+      }
+      std::vector<char> blob(sizeof(S2Desc));
+      std::memcpy(blob.data(), &d, sizeof(S2Desc));
+      op.stab = (int)P_.stabs.size();
+      P_.stabs.push_back(std::move(blob));
+      op.flops = flops;
+      op.bytes = (double)(n0 + nq) * P_.esz;
+      std::ostringstream o;
+      o << "step " << c.gates.front().step << ".." << op.step << " SWEEP2 gates=" << c.gates.size()
+        << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " C=" << (1 << d.logC)
+        << " chunks=" << d.nchunks << (direct ? " ->OUT" : "");
+      op.note = o.str();
+      P_.ops.push_back(op);
+      res.modes = c.out_modes;
+      for (int m : c.out_modes) res.ext.push_back(ext_[m]);
+      res.stride = contig_strides(res.ext);
+      res.buf = tgt;
+      res.owned = !direct;
+      if (final && !direct)
+        TQ_TRY(emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, op.step, "result->out"));
     } else {
-      ChainShape sh;
-      if (!chain_shape(c, c.out_modes, sh)) { set_error("internal: chain shape"); return TQ_ERR_INVALID; }
+      ChainShape sh = sh0;
+      if (!shape_ok) { set_error("internal: chain shape"); return TQ_ERR_INVALID; }
       const int64_t n0 = c.X0.numel();
       const int64_t nq = n0 / sh.tin_n * sh.tout_n;
       bool direct;
@@ -764,6 +1154,7 @@ class Compiler {
         sg.gtab = add_gtab(g.d.gtab);
         sg.K = (int)g.d.K;
         sg.N = (int)g.d.N;
+        sg.n = g.Sm.numel();
         sg.W = (int)count_of(w);
         sg.tab_off = entries;
         for (int64_t e = 0; e < sg.W; ++e) {
@@ -796,6 +1187,8 @@ class Compiler {
       op.store_colfast = (op.nruns > 0 && op.run_out[0] == 1 && op.run_ext[0] >= 16) ? 1 : 0;
       op.flops = flops;
       op.bytes = (double)(n0 + nq) * P_.esz;
+      op.na = n0;
+      op.nc = nq;
       std::ostringstream o;
       o << "step " << c.gates.front().step << ".." << op.step << " SWEEP gates=" << c.gates.size()
         << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " runs=" << op.nruns
@@ -930,6 +1323,10 @@ class Compiler {
     op.ldb = c.tb ? K : N; op.sB = K * N;
     op.ldc = N; op.sC = M * N;
     op.ws_bytes = gemm_workspace(P_.dtype, M, N, K, bsz);
+    op.na = bsz * M * K;
+    op.nb = bsz * K * N;
+    op.nc = bsz * M * N;
+    op.nws = (int64_t)((op.ws_bytes + P_.esz - 1) / P_.esz);
     int64_t wsoff = -1;
     if (op.ws_bytes) {
       wsoff = arenas_[region()].alloc((int64_t)op.ws_bytes);
@@ -991,12 +1388,6 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
 }
 
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
-  if (!P.side_stream) TQ_HIP(hipStreamCreateWithFlags(&P.side_stream, hipStreamNonBlocking));
-  while (P.sync_events.size() < 2) {
-    hipEvent_t e;
-    TQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    P.sync_events.push_back(e);
-  }
   if (arena || tables) {
     P.d_arena = arena;
     P.d_tables = tables;
@@ -1150,18 +1541,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     if (!accumulate && P.out_numel) TQ_HIP(hipMemsetAsync(out, 0, P.out_numel * esz, stream));
     return TQ_OK;
   }
-  // the two independent subtrees of the final step run on two streams: branch-1 ops on the side
-  // stream, forked from `stream` at every slice start and joined before the first join op
-  bool two = false;
-  for (const Op& op : P.ops) two |= op.branch == 1;
-  two = two && P.side_stream != nullptr && P.sync_events.size() >= 2;
-  hipStream_t s1 = two ? P.side_stream : stream;
   for (int64_t sl = s_begin; sl < s_end; sl += s_step) {
-    bool joined = false;
-    if (two) {
-      TQ_HIP(hipEventRecord(P.sync_events[0], stream));
-      TQ_HIP(hipStreamWaitEvent(s1, P.sync_events[0], 0));
-    }
     // decode slice id (row-major over sliced modes) -> per-input element offsets
     std::vector<int64_t> idx(ns);
     int64_t rem = sl;
@@ -1181,28 +1561,8 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       return nullptr;
     };
     const double beta_out = first ? 0.0 : 1.0;
-    for (const Op& op : P.ops) {
-      if (op.invariant && sl != s_begin) continue;  // hoisted: computed in this call's first slice
+    auto launch_one = [&](const Op& op, hipStream_t st) -> int {
       const double beta = op.writes_output ? beta_out : 0.0;
-      if (two && op.branch == 2 && !joined) {
-        TQ_HIP(hipEventRecord(P.sync_events[1], s1));
-        TQ_HIP(hipStreamWaitEvent(stream, P.sync_events[1], 0));
-        joined = true;
-      }
-      hipStream_t st = op.branch == 1 ? s1 : stream;
-      Plan::Ev ev{};
-      const bool prof = (P.profile >> op.kind) & 1;
-      if (prof) {
-        if (P.ev_free.empty()) {
-          TQ_HIP(hipEventCreate(&ev.a));
-          TQ_HIP(hipEventCreate(&ev.b));
-        } else {
-          ev = P.ev_free.back();
-          P.ev_free.pop_back();
-        }
-        ev.kind = op.kind; ev.flops = op.flops; ev.bytes = op.bytes;
-        TQ_HIP(hipEventRecord(ev.a, st));
-      }
       switch (op.kind) {
         case OP_PERMUTE:
           TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm],
@@ -1276,16 +1636,60 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           TQ_TRY(sweep_launch(P.dtype, a, st));
           break;
         }
+        default:
+          set_error("internal: op kind");
+          return TQ_ERR_INVALID;
+      }
+      return TQ_OK;
+    };
+    // one entry of the schedule: a single op, or independent sweep2 ops in one launch
+    auto launch = [&](const std::vector<int>& grp) -> int {
+      const Op& op0 = P.ops[grp[0]];
+      const int pkind = op0.kind == OP_SWEEP2 ? (int)OP_SWEEP : op0.kind;
+      Plan::Ev ev{};
+      const bool prof = (P.profile >> pkind) & 1;
+      if (prof) {
+        if (P.ev_free.empty()) {
+          TQ_HIP(hipEventCreate(&ev.a));
+          TQ_HIP(hipEventCreate(&ev.b));
+        } else {
+          ev = P.ev_free.back();
+          P.ev_free.pop_back();
+        }
+        ev.kind = pkind; ev.flops = 0; ev.bytes = 0;
+        for (int j : grp) { ev.flops += P.ops[j].flops; ev.bytes += P.ops[j].bytes; }
+        TQ_HIP(hipEventRecord(ev.a, stream));
+      }
+      if (op0.kind == OP_SWEEP2) {
+        S2Launch L;
+        L.nops = (int)grp.size();
+        int blocks = 0;
+        for (int q = 0; q < L.nops; ++q) {
+          const Op& op = P.ops[grp[q]];
+          S2Op& o = L.op[q];
+          o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[op.stab]);
+          o.X = ptr(op.a);
+          o.Y = ptr(op.c);
+          for (size_t g = 0; g < op.sgates.size(); ++g) o.G[g] = ptr(op.sgates[g].g);
+          o.block_begin = blocks;
+          o.nblocks = s2_blocks(op.s2_nchunks);
+          blocks += o.nblocks;
+          o.beta = op.writes_output ? beta_out : 0.0;
+          o.use_beta = o.beta != 0.0;
+        }
+        TQ_TRY(sweep2_launch(P.dtype, L, stream));
+      } else {
+        TQ_TRY(launch_one(op0, stream));
       }
       if (prof) {
-        TQ_HIP(hipEventRecord(ev.b, st));
+        TQ_HIP(hipEventRecord(ev.b, stream));
         P.ev_used.push_back(ev);
       }
-    }
-    if (two && !joined) {
-      TQ_HIP(hipEventRecord(P.sync_events[1], s1));
-      TQ_HIP(hipStreamWaitEvent(stream, P.sync_events[1], 0));
-    }
+      return TQ_OK;
+    };
+    if (sl == s_begin)
+      for (auto& grp : P.sched_once) TQ_TRY(launch(grp));
+    for (auto& grp : P.sched_slice) TQ_TRY(launch(grp));
     first = false;
   }
   return TQ_OK;

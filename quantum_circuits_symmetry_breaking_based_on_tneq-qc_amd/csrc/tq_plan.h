@@ -6,6 +6,7 @@
 
 #include "tq_common.h"
 #include "tq_permute.h"
+#include "tq_sweep2.h"
 
 namespace tq {
 
@@ -19,13 +20,15 @@ struct BufRef {
   int region = 0;     // compile time: arena region (branch) the offset is relative to
 };
 
-enum OpKind { OP_PERMUTE = 0, OP_GEMM = 1, OP_APPLY = 2, OP_AXPY = 3, OP_SWEEP = 4 };
+enum OpKind { OP_PERMUTE = 0, OP_GEMM = 1, OP_APPLY = 2, OP_AXPY = 3, OP_SWEEP = 4,
+              OP_SWEEP2 = 5 /* in-place butterfly sweep (profiled as OP_SWEEP) */ };
 
 // one gate of a fused sweep op (OP_SWEEP): small operand + its gather table + index table
 struct SweepGate {
   BufRef g;
   int gtab = -1;
   int K = 0, N = 0, W = 0;
+  int64_t n = 0;        // elements of the gate operand (hazard analysis)
   size_t tab_off = 0;   // entry offset of its [W][K+1] int16 table in the op's packed tables
 };
 
@@ -59,6 +62,10 @@ struct Op {
   size_t tabs_at = 0;            // byte offset of the packed gate tables inside the blob
   int tab_len = 0;
   int load_colfast = 1, store_colfast = 1;
+  // sweep2: descriptor blob = stabs[stab] (an S2Desc), launched with s2_blocks(s2_nchunks)
+  int64_t s2_nchunks = 0;
+  // element counts of a / b / c / ws (hazard analysis of the launch schedule)
+  int64_t na = 0, nb = 0, nc = 0, nws = 0;
   // bookkeeping
   int step = -1;
   double flops = 0, bytes = 0;
@@ -104,6 +111,10 @@ struct Plan {
   double flops_once = 0, bytes_once = 0;    // slice-invariant (hoisted) part
   double flops_slice = 0, bytes_slice = 0;  // per slice
   int n_gemm = 0, n_apply = 0, n_permute = 0, n_sweep = 0, n_sweep_gates = 0;
+  // launch schedule: ops grouped by dependency level; independent sweep2 ops of one level share
+  // a launch.  `once` = slice-invariant ops (first slice of an execute call), `slice` = per slice
+  std::vector<std::vector<int>> sched_once, sched_slice;
+  int n_launch_once = 0, n_launch_slice = 0;
   std::string describe;
   // hipGraph of the whole launch sequence of one execute call, replayed while the call's
   // pointers / slice range / flags are unchanged (a plan is hundreds of small launches)
@@ -129,8 +140,8 @@ struct Plan {
   std::vector<GraphEntry> graphs;
   uint64_t graph_clock = 0;
   hipStream_t cap_stream = nullptr;
-  hipStream_t side_stream = nullptr;        // branch-1 ops
-  std::vector<hipEvent_t> sync_events;      // fork / join events (reused)
+  hipStream_t side_stream = nullptr;        // (unused: independent ops share launches instead)
+  std::vector<hipEvent_t> sync_events;
   int64_t graph_builds = 0, graph_launches = 0;
 };
 

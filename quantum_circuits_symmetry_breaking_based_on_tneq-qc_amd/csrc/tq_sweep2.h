@@ -1,0 +1,79 @@
+// In-place butterfly sweep (tq_sweep2.hip): descriptors shared by the plan compiler and the
+// kernel.  A sweep op applies a chain of small operands ("gates") to a big tensor X in one HBM
+// pass, Y[outer, t_out] = (G_q o ... o G_1)(X[outer, t_in]), for chains whose modes all have
+// power-of-two extents.  Every mode bit of the working set owns a fixed *position* bit of an
+// LDS tile index; a gate reads its K inputs and writes its N outputs at the positions of its
+// index bits (outputs reuse the positions the gate frees), so the tile is updated in place.
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace tq {
+
+constexpr int kS2MaxGates = 8;
+constexpr int kS2MaxKN = 8;            // N <= 8 per gate (coefficient slots: 8 x 8)
+constexpr int kS2MaxK = 4;             // K <= 4 per gate (exact-shape gate passes)
+constexpr int kS2MaxOps = 16;          // independent sweep ops batched into one launch
+constexpr int kS2ChunkBytes = 65536;   // LDS tile per workgroup
+constexpr int kS2MaxChunkBits = 13;    // log2(chunk elements) for 8-byte elements
+constexpr int kS2MaxColBits = 48;
+constexpr int kS2LogThreads = 9;       // 512 threads per workgroup
+constexpr int kS2MaxSlots = 16;        // chunk elements per thread (load / store register slots)
+inline int s2_max_pos(int esz) { return esz > 8 ? 7 : 8; }  // tile positions (index bits)
+inline int s2_chunk_bits(int esz) { return esz > 8 ? 12 : 13; }
+
+// chunk-element code: column bits [0,13), position bits [13,21), swizzle [21,26); all XOR-combined
+constexpr int kS2CodeP = 13, kS2CodeS = 21;
+
+struct S2Gate {
+  int K = 0, N = 0;
+  uint32_t pass_mask = 0;                 // live positions the gate does not contract
+  int32_t kdep[kS2MaxKN] = {}, ndep[kS2MaxKN] = {};  // position bits of input k / output n
+  int32_t ksw[kS2MaxKN] = {}, nsw[kS2MaxKN] = {};    // their swizzle contributions
+  // LDS element-address XOR masks of input k / output n (linear in the position bits):
+  // (dep << logC) ^ (sw & (C-1))
+  int32_t kaddr[kS2MaxKN] = {}, naddr[kS2MaxKN] = {};
+  int32_t gidx[kS2MaxKN * kS2MaxKN] = {};             // coefficient k*N+n -> element of G
+};
+
+struct S2Desc {
+  int64_t ncols = 0, nchunks = 0;
+  int logC = 0, colbits = 0;     // columns per chunk (log2), column index bits
+  int nld = 0, nst = 0;          // chunk bits of the load (X) / store (Y) enumerations
+  int ngates = 0, pad = 0;
+  int64_t ld_w[16] = {}, st_w[16] = {};      // memory weight of each chunk bit (ascending)
+  int32_t ld_code[16] = {}, st_code[16] = {};
+  // LDS element address of each chunk bit: every LDS address is an XOR of these
+  int32_t ld_a[16] = {}, st_a[16] = {};
+  // register slot r (chunk bits >= kS2LogThreads of element r*512+tid): memory offset and LDS
+  // address; slots beyond the chunk repeat slot r % slots (a duplicate, harmless access)
+  int64_t ld_hm[kS2MaxSlots] = {}, st_hm[kS2MaxSlots] = {};
+  int32_t ld_ha[kS2MaxSlots] = {}, st_ha[kS2MaxSlots] = {};
+  int32_t ld_hc[kS2MaxSlots] = {}, st_hc[kS2MaxSlots] = {};
+  int64_t w_in[kS2MaxColBits] = {}, w_out[kS2MaxColBits] = {};  // column-bit weights
+  int32_t vsw[8] = {};           // swizzle vector of each position
+  S2Gate gate[kS2MaxGates];
+};
+
+struct S2Op {
+  const S2Desc* desc = nullptr;
+  const void* X = nullptr;
+  void* Y = nullptr;
+  const void* G[kS2MaxGates] = {};
+  int block_begin = 0, nblocks = 0;
+  double beta = 0.0;
+  int use_beta = 0, pad = 0;
+};
+
+struct S2Launch {
+  int nops = 0, pad = 0;
+  S2Op op[kS2MaxOps];
+};
+
+// blocks a sweep op gets when launched (chunks are strided over them)
+inline int s2_blocks(int64_t nchunks) { return (int)(nchunks < 512 ? nchunks : 512); }
+
+int sweep2_launch(int dtype, const S2Launch& L, hipStream_t stream);
+
+}  // namespace tq

@@ -1,0 +1,303 @@
+// In-place butterfly sweep: a chain of small-operand absorptions in ONE HBM pass, several
+// independent chains per launch.
+//
+// The contraction trees of the amplitude workloads (each
+// opt_einsum pairwise step at einsum_strategy.py:639-643 absorbs one (2,2,2,2) gate, or a
+// gate with an input state / output projector folded in, into a running tensor) are long
+// chains of steps that each touch a few legs.  For chains whose modes all have power-of-two
+// extents the plan compiler (tq_plan.cpp) gives every mode bit of the working set a fixed
+// position bit of a tile index; a gate with K inputs and N outputs then works on disjoint
+// groups (one assignment of the positions it does not touch): read K tile elements, write N —
+// outputs take the positions the gate frees, so the tile is updated in place and every gate
+// costs one LDS read + one LDS write per element (the table-driven sweep costs K reads).
+//
+// A workgroup owns chunks of C columns (assignments of the untouched modes) x the tile; the
+// LDS image of element (position p, column c) is p*C + (c ^ swz(p)) with a per-op linear XOR
+// swizzle chosen at plan time, so the gate passes (32 consecutive columns per half-wave) and
+// the load / store phases (elements enumerated in memory order: every half-wave touches 256
+// contiguous bytes when the tensor allows it) are LDS-bank-conflict free.  The next chunk's
+// loads are issued into registers before the current chunk's gates run.  Independent ops (the
+// two subtrees of a cut network, the tiny vector pre-absorption chains) share one launch:
+// blockIdx ranges select the op.
+//
+// Latency: the op descriptor is copied to LDS by one coalesced pass at kernel start (no chains
+// of dependent scalar loads), gate passes are instantiated per exact (K, N) (powers of two
+// K <= 4, N <= 8: no predication in the inner loop), the gate coefficients are staged once per
+// workgroup in LDS (and held in registers for small gates), and complex64 products use packed
+// FP32 FMAs (v_pk_fma_f32: 2 instead of 4 FMAs per complex multiply-add).  At most 128 VGPRs
+// per lane (launch bound), so two 512-thread workgroups share a CU.
+// Algorithmic bytes per op = (numel(X) + numel(Y)) * sizeof.
+#include <algorithm>
+#include <type_traits>
+
+#include "tq_common.h"
+#include "tq_sweep2.h"
+
+namespace tq {
+
+namespace {
+
+constexpr int NT = 512, LOG_NT = 9;
+constexpr int kLut = 128;                    // per-gate group table entries (<= 7 pass positions)
+constexpr int kCf = kS2MaxKN * kS2MaxKN;     // coefficient slots per gate
+constexpr int kDescWords = (int)(sizeof(S2Desc) / 4);
+static_assert(sizeof(S2Desc) % 4 == 0, "descriptor copy granularity");
+
+template <typename T>
+__device__ __forceinline__ T scale_add(T v, T y, double beta) {
+  if constexpr (sizeof(typename Traits<T>::R) == 4) return v + y * (float)beta;
+  else return v + y * beta;
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// uniform base + zero-extended 32-bit lane byte offset: global_load/store with an SGPR-pair base
+// and one VGPR offset shared by every register slot (no 64-bit VGPR address per slot)
+template <typename T>
+__device__ __forceinline__ T* lane_at(T* base, uint32_t byte_off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off);
+}
+template <typename T>
+__device__ __forceinline__ const T* lane_at(const T* base, uint32_t byte_off) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+// acc += a * b on packed f32: (a.re, a.re) * (b.re, b.im) + (a.im, a.im) * (-b.im, b.re).
+// The broadcasts and the swap / negation are operand modifiers (op_sel / neg), not copies.
+__device__ __forceinline__ f2v pmac(f2v acc, f2v a, f2v b) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "+v"(acc) : "v"(a), "v"(b));
+  return acc;
+}
+
+template <typename T>
+__device__ __forceinline__ void mac(T& acc, const T& a, const T& b) {
+  if constexpr (std::is_same<T, c64>::value) {
+    const f2v r = pmac(f2v{acc.re, acc.im}, f2v{a.re, a.im}, f2v{b.re, b.im});
+    acc = c64{r.x, r.y};
+  } else {
+    cmac(acc, a, b);
+  }
+}
+
+// One gate over all groups of the chunk.  Every LDS address is an XOR of contributions:
+// group (lut[pp] ^ c) ^ input k (kaddr[k]) / output n (naddr[n]).  U groups per thread in
+// flight; all K inputs of a group are read before any of its N outputs is written (outputs
+// reuse the input positions).
+template <typename T, int K, int N>
+__device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restrict__ cf,
+                                          const S2Gate* __restrict__ gt,
+                                          const int32_t* __restrict__ lut, int logC) {
+  constexpr int U = sizeof(T) > 8 ? (K * N >= 8 ? 1 : 2) : (K * N >= 16 ? 2 : 4);
+  constexpr bool kReg = K * N * sizeof(T) <= 64;   // coefficients held in registers
+  const int tid = threadIdx.x;
+  const int ngroups = (1 << logC) << __popc(gt->pass_mask);
+  const int cm = (1 << logC) - 1;
+  int ka[K], na[N];
+#pragma unroll
+  for (int k = 0; k < K; ++k) ka[k] = gt->kaddr[k];
+#pragma unroll
+  for (int n = 0; n < N; ++n) na[n] = gt->naddr[n];
+  T creg[kReg ? K * N : 1];
+  if constexpr (kReg) {
+#pragma unroll
+    for (int i = 0; i < K * N; ++i) creg[i] = cf[i];
+  }
+  for (int g0 = tid; g0 < ngroups; g0 += U * NT) {
+    // keeps the compiler from hoisting the (loop-invariant) LDS coefficient reads of large gates
+    // out of the loop, which would pin K*N coefficients in registers
+    if constexpr (!kReg) asm volatile("" ::: "memory");
+    int a0[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int gi = g0 + u * NT;
+      ok[u] = gi < ngroups;
+      gi = ok[u] ? gi : g0;
+      a0[u] = lut[gi >> logC] ^ (gi & cm);
+    }
+    T x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < K; ++k) x[u][k] = buf[a0[u] ^ ka[k]];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      T c[K];
+      if constexpr (kReg) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) c[k] = creg[k * N + n];
+      } else {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < K; ++k) c[k] = cf[k * N + n];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        T acc = tzero<T>();
+#pragma unroll
+        for (int k = 0; k < K; ++k) mac(acc, x[u][k], c[k]);
+        if (ok[u]) buf[a0[u] ^ na[n]] = acc;
+      }
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void run_gate(T* buf, const T* cf, const S2Gate* gt, const int32_t* lut,
+                                         int logC) {
+#define TQ_GATE(k, n) \
+  case k * 16 + n: gate_pass<T, k, n>(buf, cf, gt, lut, logC); break;
+  switch (gt->K * 16 + gt->N) {
+    TQ_GATE(1, 1) TQ_GATE(1, 2) TQ_GATE(1, 4) TQ_GATE(1, 8)
+    TQ_GATE(2, 1) TQ_GATE(2, 2) TQ_GATE(2, 4) TQ_GATE(2, 8)
+    TQ_GATE(4, 1) TQ_GATE(4, 2) TQ_GATE(4, 4) TQ_GATE(4, 8)
+    default: break;   // the plan compiler only emits K in {1, 2, 4}, N in {1, 2, 4, 8}
+  }
+#undef TQ_GATE
+}
+
+template <typename T, int CB>
+__global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
+  constexpr int RMAX = (1 << CB) / NT;
+  static_assert(RMAX <= kS2MaxSlots, "register slots");
+  __shared__ T buf[1 << CB];
+  __shared__ int32_t lut[kS2MaxGates * kLut];            // group -> LDS address part
+  __shared__ T cf[kS2MaxGates * kCf];                    // gate coefficients, k*N+n
+  const int tid = threadIdx.x;
+  // ---- which op this workgroup works on (wave-uniform scan over <= 16 ranges)
+  int j = 0;
+  for (int q = 1; q < L.nops; ++q)
+    if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
+  const S2Op& op = L.op[j];
+  const S2Desc* __restrict__ d = op.desc;
+  const T* __restrict__ X = reinterpret_cast<const T*>(op.X);
+  T* __restrict__ Y = reinterpret_cast<T*>(op.Y);
+  const int lb = (int)blockIdx.x - op.block_begin, nb = op.nblocks;
+  const int logC = d->logC, colbits = d->colbits, ngates = d->ngates;
+  const int cm = (1 << logC) - 1;
+  const int64_t nchunks = d->nchunks;
+  const int nld = d->nld, nst = d->nst;
+  const int nin = 1 << nld, nout = 1 << nst;
+  const int rin = (nin + NT - 1) / NT, rout = (nout + NT - 1) / NT;  // slots in use (powers of 2)
+  const bool use_beta = op.use_beta;
+  const double beta = op.beta;
+  // ---- gate coefficients -> LDS (one wave per gate)
+  {
+    const int g = tid >> 6, t = tid & 63;
+    if (g < ngates) {
+      const S2Gate& gt = d->gate[g];
+      if (t < gt.K * gt.N) cf[g * kCf + t] = reinterpret_cast<const T*>(op.G[g])[gt.gidx[t]];
+    }
+  }
+  // ---- group tables -> LDS: LDS address part (positions << logC) ^ swizzle of group pp
+  for (int g = 0; g < ngates; ++g) {
+    const uint32_t mask = d->gate[g].pass_mask;
+    if (tid < (1 << __popc(mask))) {
+      int base = 0, sw = 0;
+      uint32_t m = mask;
+      for (int t = 0; m; ++t) {
+        const int lo = __builtin_ctz(m);
+        m &= m - 1;
+        if ((tid >> t) & 1) { base |= 1 << lo; sw ^= d->vsw[lo]; }
+      }
+      lut[g * kLut + tid] = (base << logC) ^ (sw & cm);
+    }
+  }
+  // ---- per-thread part of the load / store enumerations (low LOG_NT chunk bits); threads
+  // beyond a small chunk duplicate element tid % n (same value to the same place)
+  int64_t ldm = 0, stm = 0;
+  int lda = 0, sta = 0;
+  {
+    const int ti = tid & (nin - 1), to = tid & (nout - 1);
+    for (int b = 0; b < LOG_NT; ++b) {
+      if (b < nld && ((ti >> b) & 1)) { ldm += d->ld_w[b]; lda ^= d->ld_a[b]; }
+      if (b < nst && ((to >> b) & 1)) { stm += d->st_w[b]; sta ^= d->st_a[b]; }
+    }
+  }
+  const bool st_lane = tid < nout;
+  // uniform part (chunk + register slot) in scalar registers, lane part as a 32-bit byte offset
+  const uint32_t ldo = (uint32_t)(ldm * (int64_t)sizeof(T)), sto = (uint32_t)(stm * (int64_t)sizeof(T));
+  __syncthreads();
+  auto chunk_base = [&](int64_t ch, const int64_t* w) {
+    int64_t o = 0;
+    for (int b = logC; b < colbits; ++b)
+      if ((ch >> (b - logC)) & 1) o += w[b];
+    return o;
+  };
+  T reg[RMAX];
+  // slot loops run a compile-time count (a power of two): loads / LDS accesses issue back to back
+#define TQ_SLOTS(R, BODY)                                  \
+  if constexpr (RMAX >= (R)) {                             \
+    _Pragma("unroll") for (int r = 0; r < (R); ++r) BODY;  \
+  }
+#define TQ_BY_COUNT(n, BODY)                                     \
+  do {                                                           \
+    if ((n) >= 16) { TQ_SLOTS(16, BODY) }                        \
+    else if ((n) >= 8) { TQ_SLOTS(8, BODY) }                     \
+    else if ((n) >= 4) { TQ_SLOTS(4, BODY) }                     \
+    else if ((n) >= 2) { TQ_SLOTS(2, BODY) }                     \
+    else { TQ_SLOTS(1, BODY) }                                   \
+  } while (0)
+  auto prefetch = [&](int64_t ch) {
+    const int64_t base = chunk_base(ch, d->w_in);
+    TQ_BY_COUNT(rin, reg[r] = *lane_at(X + base + d->ld_hm[r], ldo));
+  };
+  int64_t ch = lb;
+  if (ch < nchunks) prefetch(ch);
+  for (; ch < nchunks; ch += nb) {
+    TQ_BY_COUNT(rin, buf[lda ^ d->ld_ha[r]] = reg[r]);
+    __syncthreads();
+    for (int g = 0; g < ngates; ++g) {
+      run_gate<T>(buf, cf + g * kCf, &d->gate[g], lut + g * kLut, logC);
+      __syncthreads();
+    }
+    const int64_t base = chunk_base(ch, d->w_out);
+    // LDS -> the same registers -> HBM; then the next chunk's loads (they fly with these stores
+    // and with the other workgroup's gates on this CU)
+    TQ_BY_COUNT(rout, reg[r] = buf[sta ^ d->st_ha[r]]);
+    if (st_lane) {
+      if (use_beta) {
+        TQ_BY_COUNT(rout, { T* p = lane_at(Y + base + d->st_hm[r], sto); *p = scale_add(reg[r], *p, beta); });
+      } else {
+        TQ_BY_COUNT(rout, *lane_at(Y + base + d->st_hm[r], sto) = reg[r]);
+      }
+    }
+    const int64_t nxt = ch + nb;
+    if (nxt < nchunks) prefetch(nxt);
+    __syncthreads();  // the tile is rewritten by the next chunk
+  }
+#undef TQ_BY_COUNT
+#undef TQ_SLOTS
+}
+
+template <typename T>
+int launch_t(const S2Launch& L, hipStream_t stream) {
+  constexpr int CB = sizeof(T) > 8 ? 12 : 13;
+  int blocks = 0;
+  for (int q = 0; q < L.nops; ++q) blocks = std::max(blocks, L.op[q].block_begin + L.op[q].nblocks);
+  if (blocks <= 0) return TQ_OK;
+  hipLaunchKernelGGL((sweep2_kernel<T, CB>), dim3((unsigned)blocks), dim3(NT), 0, stream, L);
+  TQ_HIP(hipGetLastError());
+  return TQ_OK;
+}
+
+}  // namespace
+
+int sweep2_launch(int dtype, const S2Launch& L, hipStream_t stream) {
+  if (L.nops < 1 || L.nops > kS2MaxOps) {
+    set_error("sweep2: bad op count");
+    return TQ_ERR_INVALID;
+  }
+  switch (dtype) {
+    case TQ_F32: return launch_t<float>(L, stream);
+    case TQ_F64: return launch_t<double>(L, stream);
+    case TQ_C64: return launch_t<c64>(L, stream);
+    case TQ_C128: return launch_t<c128>(L, stream);
+  }
+  set_error("sweep2: bad dtype");
+  return TQ_ERR_INVALID;
+}
+
+}  // namespace tq
