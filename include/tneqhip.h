@@ -27,6 +27,10 @@
  *                       (einsum_strategy.py:622-643), plus index slicing.
  *   tq_axpy           — the partial-amplitude accumulation before the slice reduce
  *                       (AllReduceGrad, tneq_qc/distributed/optim/allreduce_grad.py:13-60).
+ *   tq_hermite_features — EngineSiamese.generate_data and its helpers _init_mx_weights /
+ *                       _eval_hermitenorm_batch(_np) (tneq_qc/core/engine_siamese.py:59-254).
+ *   tq_inverse_cdf_sample — the clamp / cumsum / normalise / search / interpolate block of
+ *                       EngineSiamese.sample (tneq_qc/core/engine_siamese.py:854-905).
  */
 #ifndef TNEQHIP_H
 #define TNEQHIP_H
@@ -133,6 +137,29 @@ enum { TQ_OP_PERMUTE = 0, TQ_OP_GEMM = 1, TQ_OP_APPLY = 2, TQ_OP_AXPY = 3, TQ_OP
 int tq_plan_profile(tq_plan plan, int enable);
 int tq_plan_profile_read(tq_plan plan, int op_kind, double* total_ms, int64_t* launches,
                          double* flops, double* bytes);
+
+/* ---- measurement data (EngineSiamese) ---------------------------------------------- */
+#define TQ_HERMITE_MAX_K 128
+#define TQ_ICDF_MAX_GRID 8192
+
+/* Hermite measurement data of n_points scalar inputs x (float64, device):
+ *   phi[p][k]   = (w_k * sqrt(exp(-x_p^2 / 2))) * He_k(x_p)   (k < K; probabilists' Hermite)
+ *   mx[p][k][l] = conj(phi[p][k]) * phi[p][l]
+ * weights: HOST array of K float64 w_k, copied into the launch arguments.  1 <= K <=
+ * TQ_HERMITE_MAX_K.  A complex dtype computes in float64 and rounds once
+ * (engine_siamese.py:165-207); a real dtype computes in its own precision (:212-254).
+ * phi ([n_points][K]) or mx ([n_points][K][K]) may be NULL.                              */
+int tq_hermite_features(int dtype, int64_t n_points, int K, const double* x, const double* weights,
+                        void* phi, void* mx, void* stream);
+
+/* One inverse-CDF draw per row of a real density (dtype TQ_F32 / TQ_F64; row s at
+ * density + s * ld_density) on grid_x (grid_size points, 2 <= grid_size <= TQ_ICDF_MAX_GRID):
+ * clamp at 0, inclusive prefix sum, normalise by (total + 1e-10), idx = min(#(cdf < u[s]),
+ * grid_size - 2), linear interpolation between grid points idx and idx + 1 into
+ * samples[s * samples_stride].  u: n_rows float32 uniforms (device).                       */
+int tq_inverse_cdf_sample(int dtype, int64_t n_rows, int64_t grid_size, const void* density,
+                          int64_t ld_density, const void* grid_x, const float* u, void* samples,
+                          int64_t samples_stride, void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,8 +23,9 @@ EXPORTED = (
     "tq_gemm_batched",
     "tq_gemm_workspace_size", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
     "tq_plan_create", "tq_plan_query", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
-    "tq_plan_profile", "tq_plan_profile_read",
+    "tq_plan_profile", "tq_plan_profile_read", "tq_hermite_features", "tq_inverse_cdf_sample",
 )
+TQ_HERMITE_MAX_K, TQ_ICDF_MAX_GRID = 128, 8192
 TQ_OP_PERMUTE, TQ_OP_GEMM, TQ_OP_APPLY, TQ_OP_AXPY, TQ_OP_SWEEP = 0, 1, 2, 3, 4
 
 
@@ -66,6 +67,10 @@ _SIGS = {
     "tq_plan_profile": (_c.c_int, [_vp, _c.c_int]),
     "tq_plan_profile_read": (_c.c_int, [_vp, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64),
                                         _c.POINTER(_c.c_double), _c.POINTER(_c.c_double)]),
+    "tq_hermite_features": (_c.c_int, [_c.c_int, _c.c_int64, _c.c_int, _vp, _c.POINTER(_c.c_double), _vp,
+                                       _vp, _vp]),
+    "tq_inverse_cdf_sample": (_c.c_int, [_c.c_int, _c.c_int64, _c.c_int64, _vp, _c.c_int64, _vp, _vp, _vp,
+                                         _c.c_int64, _vp]),
 }
 
 

@@ -234,6 +234,34 @@ int tq_plan_profile_read(tq_plan p, int op_kind, double* total_ms, int64_t* laun
   TQ_GUARD_END
 }
 
+int tq_hermite_features(int dtype, int64_t n_points, int K, const double* x, const double* weights,
+                        void* phi, void* mx, void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(tq::dtype_valid(dtype), "dtype");
+  TQ_CHECK_ARG(K >= 1 && K <= TQ_HERMITE_MAX_K, "K must be in [1, TQ_HERMITE_MAX_K]");
+  TQ_CHECK_ARG(n_points >= 0, "n_points < 0");
+  TQ_CHECK_ARG(weights != nullptr, "null weights");
+  TQ_CHECK_ARG(n_points == 0 || x != nullptr, "null x");
+  TQ_CHECK_ARG(phi != nullptr || mx != nullptr, "neither phi nor mx requested");
+  return tq::hermite_launch(dtype, n_points, K, x, weights, phi, mx, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+int tq_inverse_cdf_sample(int dtype, int64_t n_rows, int64_t grid_size, const void* density,
+                          int64_t ld_density, const void* grid_x, const float* u, void* samples,
+                          int64_t samples_stride, void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(dtype == TQ_F32 || dtype == TQ_F64, "density must be real (TQ_F32 / TQ_F64)");
+  TQ_CHECK_ARG(grid_size >= 2 && grid_size <= TQ_ICDF_MAX_GRID,
+               "grid_size must be in [2, TQ_ICDF_MAX_GRID]");
+  TQ_CHECK_ARG(n_rows >= 0 && n_rows <= INT32_MAX, "n_rows out of range");
+  TQ_CHECK_ARG(ld_density >= grid_size, "ld_density < grid_size");
+  TQ_CHECK_ARG(n_rows == 0 || (density && grid_x && u && samples), "null pointer");
+  return tq::icdf_launch(dtype, n_rows, grid_size, density, ld_density, grid_x, u, samples,
+                         samples_stride, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
 int tq_plan_destroy(tq_plan p) {
   if (!p) return TQ_OK;
   tq::plan_release(p->plan);

@@ -102,5 +102,11 @@ int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_
                  const void* S, const void* G, const int32_t* gidx, void* C, double beta,
                  hipStream_t stream);
 int axpy_launch(int dtype, int64_t n, const void* x, void* y, double beta, hipStream_t stream);
+// measurement data (tq_data.hip)
+int hermite_launch(int dtype, int64_t n, int K, const double* x, const double* w, void* phi,
+                   void* mx, hipStream_t stream);
+int icdf_launch(int dtype, int64_t rows, int64_t grid_size, const void* density, int64_t ld,
+                const void* grid_x, const float* u, void* out, int64_t out_stride,
+                hipStream_t stream);
 
 }  // namespace tq

@@ -643,20 +643,37 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
   auto aligned = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   g.vecA = aligned(A) && lda % VE == 0 && (batch == 1 || sA % VE == 0);
   g.vecB = aligned(B) && ldb % VE == 0 && (batch == 1 || sB % VE == 0);
-  if ((int64_t)g.mt * g.nt > INT32_MAX || batch * splits > 65535) {
+  if ((int64_t)g.mt * g.nt > INT32_MAX) {
     set_error("gemm: grid too large");
     return TQ_ERR_UNSUPPORTED;
   }
-  dim3 grid(g.mt * g.nt, 1, (unsigned)(batch * splits));
-#define TQ_GEMM_CASE(ta, tb)                                                              \
-  if (transA == ta && transB == tb) {                                                     \
-    hipLaunchKernelGGL((gemm_kernel<R, CPLX, ta, tb>), grid, dim3(kThreads), 0, stream, g); \
+  // grid.z holds batch x splits (<= 65535): larger batches (e.g. the S*G measurement batch of
+  // EngineSiamese.sample) run as several launches over batch ranges (split-K is 1 there: such
+  // batches already give >= 512 tiles)
+  const int64_t bchunk = splits > 1 ? batch : std::min<int64_t>(batch, 65535);
+  if (bchunk * splits > 65535) {
+    set_error("gemm: grid too large");
+    return TQ_ERR_UNSUPPORTED;
   }
-  TQ_GEMM_CASE(0, 0)
-  TQ_GEMM_CASE(0, 1)
-  TQ_GEMM_CASE(1, 0)
-  TQ_GEMM_CASE(1, 1)
+  const size_t esz = (size_t)EW * sizeof(R);
+  for (int64_t b0 = 0; b0 < batch; b0 += bchunk) {
+    const int64_t nb = std::min<int64_t>(bchunk, batch - b0);
+    GemmArgs gb = g;
+    gb.A = (const char*)A + (size_t)(b0 * sA) * esz;
+    gb.B = (const char*)B + (size_t)(b0 * sB) * esz;
+    gb.C = (char*)C + (size_t)(b0 * sC) * esz;
+    gb.batch = nb;
+    dim3 grid(g.mt * g.nt, 1, (unsigned)(nb * splits));
+#define TQ_GEMM_CASE(ta, tb)                                                               \
+    if (transA == ta && transB == tb) {                                                    \
+      hipLaunchKernelGGL((gemm_kernel<R, CPLX, ta, tb>), grid, dim3(kThreads), 0, stream, gb); \
+    }
+    TQ_GEMM_CASE(0, 0)
+    TQ_GEMM_CASE(0, 1)
+    TQ_GEMM_CASE(1, 0)
+    TQ_GEMM_CASE(1, 1)
 #undef TQ_GEMM_CASE
+  }
   TQ_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t total = batch * M * N * EW;

@@ -3,13 +3,16 @@
 These are the device primitives the backend and the contraction plans are built from:
 ``permute`` (reference: BackendPyTorch.permute, tneq_qc/backends/backend_pytorch.py:619-621),
 ``gemm`` (the GEMM under every tensordot), ``contract_pair`` (one pairwise einsum,
-BackendPyTorch.einsum with two operands, backend_pytorch.py:623-625).
+BackendPyTorch.einsum with two operands, backend_pytorch.py:623-625), and the measurement-data
+kernels of EngineSiamese: ``hermite_features`` (generate_data, engine_siamese.py:133-254) and
+``inverse_cdf_sample`` (the CDF block of sample, engine_siamese.py:854-905).
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Sequence
+from typing import Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -139,3 +142,55 @@ def axpy(x: torch.Tensor, y: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
                             ctypes.c_void_p(y.data_ptr()), float(beta), ctypes.c_void_p(_stream_ptr(dev)))
     check(rc, "tq_axpy")
     return y
+
+
+def hermite_features(x: torch.Tensor, K: int, weights, dtype: torch.dtype, want_phi: bool = True):
+    """Hermite measurement data of every entry of ``x`` (any shape; the real part is used):
+    ``phi[..., k] = (w_k * sqrt(exp(-x^2/2))) * He_k(x)`` and ``mx[..., k, l] = conj(phi_k) phi_l``
+    in ``dtype``; complex dtypes compute in float64, real dtypes in their own precision
+    (engine_siamese.py:133-254).  ``weights``: host array of at least K float64 w_k.
+    Returns (phi or None, mx)."""
+    dev = _require_device(x)
+    K = int(K)
+    if not 1 <= K <= _lib.TQ_HERMITE_MAX_K:
+        raise ValueError(f"K must be in [1, {_lib.TQ_HERMITE_MAX_K}], got {K}")
+    w = np.ascontiguousarray(np.asarray(weights, dtype=np.float64).reshape(-1)[:K])
+    if w.shape[0] < K:
+        raise ValueError(f"need {K} Hermite weights, got {w.shape[0]}")
+    xd = (x.real if x.is_complex() else x).to(torch.float64).contiguous()
+    phi = torch.empty(tuple(x.shape) + (K,), dtype=dtype, device=dev) if want_phi else None
+    mx = torch.empty(tuple(x.shape) + (K, K), dtype=dtype, device=dev)
+    rc = _lib.lib().tq_hermite_features(dtype_code(dtype), xd.numel(), K, ctypes.c_void_p(xd.data_ptr()),
+                                        w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        ctypes.c_void_p(phi.data_ptr() if phi is not None else None),
+                                        ctypes.c_void_p(mx.data_ptr()), ctypes.c_void_p(_stream_ptr(dev)))
+    check(rc, "tq_hermite_features")
+    return phi, mx
+
+
+def inverse_cdf_sample(density: torch.Tensor, grid: torch.Tensor, u: torch.Tensor,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One inverse-CDF draw per row of a real (S, G) density on a (G,) grid with S float32
+    uniforms ``u`` (engine_siamese.py:857-905): clamp >= 0, cumsum, / (total + 1e-10),
+    idx = min(#(cdf < u), G - 2), linear interpolation.  Returns (S,) in the density's dtype."""
+    if density.ndim != 2 or grid.ndim != 1 or grid.shape[0] != density.shape[1]:
+        raise ValueError(f"density must be (S, G) and grid (G,), got {tuple(density.shape)} and {tuple(grid.shape)}")
+    if density.dtype not in (torch.float32, torch.float64):
+        raise ValueError(f"density must be real float32/float64, got {density.dtype}")
+    dev = _require_device(density, grid)
+    S, G = density.shape
+    d = density.contiguous()
+    gr = grid.contiguous()
+    uu = u.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
+    if uu.numel() != S:
+        raise ValueError(f"need {S} uniforms, got {uu.numel()}")
+    if out is None:
+        out = torch.empty(S, dtype=density.dtype, device=dev)
+    elif out.shape != (S,) or out.dtype != density.dtype or out.device != dev:
+        raise ValueError("out must be an (S,) tensor of the density's dtype on its device")
+    rc = _lib.lib().tq_inverse_cdf_sample(dtype_code(density.dtype), S, G, ctypes.c_void_p(d.data_ptr()), G,
+                                          ctypes.c_void_p(gr.data_ptr()), ctypes.c_void_p(uu.data_ptr()),
+                                          ctypes.c_void_p(out.data_ptr()), out.stride(0),
+                                          ctypes.c_void_p(_stream_ptr(dev)))
+    check(rc, "tq_inverse_cdf_sample")
+    return out
