@@ -328,10 +328,10 @@ __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
 //  * split-K over the grid (slab reduce kernel below); a bijective XCD remap puts all tiles of one
 //    K-split on one XCD so each XCD's L2 streams its K range of A and B from HBM exactly once.
 namespace fastc64 {
-constexpr int BK = 16, NSTAGE = 3;
-// block configuration: WMW x WNW waves, each owning TI x TJ tiles of 32 x 32 outputs
-template <int WMW_, int WNW_, int TI_, int TJ_> struct Tile {
-  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_;
+// block configuration: WMW x WNW waves, each owning TI x TJ tiles of 32 x 32 outputs; K-tiles
+// of BK rows in an NS-stage LDS ring (NS - 1 tiles in flight)
+template <int WMW_, int WNW_, int TI_, int TJ_, int BK_ = 16, int NS_ = 3> struct Tile {
+  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_, BK = BK_, NS = NS_;
   static constexpr int NW = WMW * WNW, NT = 64 * NW;
   static constexpr int WM = 32 * TI, WN = 32 * TJ;            // wave tile
   static constexpr int BM = WMW * WM, BN = WNW * WN;           // block tile
@@ -361,13 +361,18 @@ struct FastArgs {
   float beta;
 };
 
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 // G3M: Gauss's 3-multiplication complex product (P1 = Ar Br, P2 = Ai Bi, P3 = (Ar+Ai)(Br+Bi);
 // Cr = P1 - P2, Ci = P3 - P1 - P2): 3 real MFMAs per complex k-step instead of 4, all in f32.
 template <bool G3M, typename TL>
 __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) {
   using namespace fastc64;
   constexpr int BM = TL::BM, BN = TL::BN, WMW = TL::WMW, TI = TL::TI, TJ = TL::TJ;
-  constexpr int STAGE = TL::STAGE, A_FLOATS = TL::A_FLOATS;
+  constexpr int STAGE = TL::STAGE, A_FLOATS = TL::A_FLOATS, BK = TL::BK, NSTAGE = TL::NS;
   constexpr int A_PIECES_PER_WAVE = TL::A_PIECES_PER_WAVE, B_PIECES_PER_WAVE = TL::B_PIECES_PER_WAVE;
   constexpr int NACC = G3M ? 3 : 2;
   __shared__ __attribute__((aligned(16))) float lds[NSTAGE * STAGE];
@@ -436,19 +441,13 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
   const int a_off = (fk * BM + wm * TL::WM + fr) * 2;
   const int b_off = A_FLOATS + (fk * BN + wn * TL::WN + fr) * 2;
 
-  issue(0, 0);
-  if (nkt > 1) issue(1, 1);
+  for (int p = 0; p < NSTAGE - 1 && p < nkt; ++p) issue(p, p);
   for (int t = 0; t < nkt; ++t) {
-    if (t + 1 < nkt) {
-      if constexpr (TL::NDMA == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if constexpr (TL::NDMA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if constexpr (TL::NDMA == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else static_assert(TL::NDMA == 4 || TL::NDMA == 6 || TL::NDMA == 8, "vmcnt");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // tile t must have landed; tiles t+1 .. t+NSTAGE-2 may stay in flight (counted waits only)
+    if (NSTAGE > 2 && t + 1 < nkt) vm_wait<TL::NDMA * (NSTAGE > 2 ? NSTAGE - 2 : 0)>();
+    else vm_wait<0>();
     asm volatile("s_barrier" ::: "memory");
-    if (t + 2 < nkt) issue(t + 2, (t + 2) % NSTAGE);
+    if (t + NSTAGE - 1 < nkt) issue(t + NSTAGE - 1, (t + NSTAGE - 1) % NSTAGE);
     const float* s = lds + (t % NSTAGE) * STAGE;
     // fragments of k-step kk+2 are read while the MFMAs of k-step kk run
     float2 a[TI], bb[TJ];
@@ -545,7 +544,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
 // eligibility and split choice of the fast path (shared by launch and workspace sizing)
 template <typename TL>
 int fast_c64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
-  using namespace fastc64;
+  constexpr int BK = TL::BK;
   if (!(transA == 1 && transB == 0)) return 0;
   if (M % TL::BM || N % TL::BN || K % BK || K == 0) return 0;
   const int64_t tiles = (M / TL::BM) * (N / TL::BN) * batch;
@@ -556,8 +555,8 @@ int fast_c64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, i
   return s;
 }
 int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
-  return gemm_3m() ? fast_c64_splits_t<fastc64::Tile3M>(transA, transB, M, N, K, batch)
-                   : fast_c64_splits_t<fastc64::Tile4M>(transA, transB, M, N, K, batch);
+  if (!gemm_3m()) return fast_c64_splits_t<fastc64::Tile4M>(transA, transB, M, N, K, batch);
+  return fast_c64_splits_t<fastc64::Tile3M>(transA, transB, M, N, K, batch);
 }
 
 // C_b = sum_s W[s][b] + beta * C_b

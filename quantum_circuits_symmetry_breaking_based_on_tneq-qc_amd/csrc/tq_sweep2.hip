@@ -16,7 +16,7 @@
 // swizzle chosen at plan time, so the gate passes (32 consecutive columns per half-wave) and
 // the load / store phases (elements enumerated in memory order: every half-wave touches 256
 // contiguous bytes when the tensor allows it) are LDS-bank-conflict free.  The next chunk's
-// loads are issued into registers before the current chunk's gates run.  Independent ops (the
+// loads are issued into registers before the current chunk's stores.  Independent ops (the
 // two subtrees of a cut network, the tiny vector pre-absorption chains) share one launch:
 // blockIdx ranges select the op.
 //
@@ -254,18 +254,35 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       __syncthreads();
     }
     const int64_t base = chunk_base(ch, d->w_out);
-    // LDS -> the same registers -> HBM; then the next chunk's loads (they fly with these stores
-    // and with the other workgroup's gates on this CU)
-    TQ_BY_COUNT(rout, reg[r] = buf[sta ^ d->st_ha[r]]);
-    if (st_lane) {
-      if (use_beta) {
-        TQ_BY_COUNT(rout, { T* p = lane_at(Y + base + d->st_hm[r], sto); *p = scale_add(reg[r], *p, beta); });
-      } else {
-        TQ_BY_COUNT(rout, *lane_at(Y + base + d->st_hm[r], sto) = reg[r]);
-      }
-    }
+    // the next chunk's loads go out first (the wait for them at the top of the next iteration
+    // then leaves this chunk's stores in flight); the tile leaves LDS in batches of 4 register
+    // slots, each batch stored before the next is read (keeps the register budget)
     const int64_t nxt = ch + nb;
     if (nxt < nchunks) prefetch(nxt);
+    if (rout >= 4) {
+      for (int r0 = 0; r0 < rout; r0 += 4) {
+        T t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ d->st_ha[r0 + q]];
+        if (st_lane) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            T* p = lane_at(Y + base + d->st_hm[r0 + q], sto);
+            *p = use_beta ? scale_add(t[q], *p, beta) : t[q];
+          }
+        }
+        asm volatile("" ::: "memory");
+      }
+    } else {
+      T t[4];
+      TQ_BY_COUNT(rout, t[r] = buf[sta ^ d->st_ha[r]]);
+      if (st_lane) {
+        TQ_BY_COUNT(rout, {
+          T* p = lane_at(Y + base + d->st_hm[r], sto);
+          *p = use_beta ? scale_add(t[r], *p, beta) : t[r];
+        });
+      }
+    }
     __syncthreads();  // the tile is rewritten by the next chunk
   }
 #undef TQ_BY_COUNT
