@@ -40,8 +40,18 @@ namespace {
 constexpr int NT = 512, LOG_NT = 9;
 constexpr int kLut = 128;                    // per-gate group table entries (<= 7 pass positions)
 constexpr int kCf = kS2MaxKN * kS2MaxKN;     // coefficient slots per gate
-constexpr int kDescWords = (int)(sizeof(S2Desc) / 4);
-static_assert(sizeof(S2Desc) % 4 == 0, "descriptor copy granularity");
+// per-gate fields the gate passes read, staged in LDS: read in every pass of every chunk, they
+// must not queue behind the chunk's HBM stores (descriptor loads are vector loads)
+constexpr int kGmK = 0, kGmN = 1, kGmPass = 2, kGmKaddr = 3, kGmNaddr = kGmKaddr + kS2MaxK;
+constexpr int kGm = 16;
+
+// per-chunk tables of the load / store phases, staged in LDS for the same reason
+struct S2Hot {
+  int64_t ld_hm[kS2MaxSlots], st_hm[kS2MaxSlots];
+  int64_t w_in[kS2MaxColBits], w_out[kS2MaxColBits];
+  int32_t ld_ha[kS2MaxSlots], st_ha[kS2MaxSlots];
+};
+static_assert(kGmNaddr + kS2MaxKN <= kGm, "gate meta layout");
 
 template <typename T>
 __device__ __forceinline__ T scale_add(T v, T y, double beta) {
@@ -87,18 +97,18 @@ __device__ __forceinline__ void mac(T& acc, const T& a, const T& b) {
 // reuse the input positions).
 template <typename T, int K, int N>
 __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restrict__ cf,
-                                          const S2Gate* __restrict__ gt,
+                                          const int32_t* __restrict__ gm,
                                           const int32_t* __restrict__ lut, int logC) {
   constexpr int U = sizeof(T) > 8 ? (K * N >= 8 ? 1 : 2) : (K * N >= 16 ? 2 : 4);
   constexpr bool kReg = K * N * sizeof(T) <= 64;   // coefficients held in registers
   const int tid = threadIdx.x;
-  const int ngroups = (1 << logC) << __popc(gt->pass_mask);
+  const int ngroups = (1 << logC) << __popc((uint32_t)gm[kGmPass]);
   const int cm = (1 << logC) - 1;
   int ka[K], na[N];
 #pragma unroll
-  for (int k = 0; k < K; ++k) ka[k] = gt->kaddr[k];
+  for (int k = 0; k < K; ++k) ka[k] = gm[kGmKaddr + k];
 #pragma unroll
-  for (int n = 0; n < N; ++n) na[n] = gt->naddr[n];
+  for (int n = 0; n < N; ++n) na[n] = gm[kGmNaddr + n];
   T creg[kReg ? K * N : 1];
   if constexpr (kReg) {
 #pragma unroll
@@ -145,11 +155,11 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
 }
 
 template <typename T>
-__device__ __forceinline__ void run_gate(T* buf, const T* cf, const S2Gate* gt, const int32_t* lut,
+__device__ __forceinline__ void run_gate(T* buf, const T* cf, const int32_t* gm, const int32_t* lut,
                                          int logC) {
 #define TQ_GATE(k, n) \
-  case k * 16 + n: gate_pass<T, k, n>(buf, cf, gt, lut, logC); break;
-  switch (gt->K * 16 + gt->N) {
+  case k * 16 + n: gate_pass<T, k, n>(buf, cf, gm, lut, logC); break;
+  switch (gm[kGmK] * 16 + gm[kGmN]) {
     TQ_GATE(1, 1) TQ_GATE(1, 2) TQ_GATE(1, 4) TQ_GATE(1, 8)
     TQ_GATE(2, 1) TQ_GATE(2, 2) TQ_GATE(2, 4) TQ_GATE(2, 8)
     TQ_GATE(4, 1) TQ_GATE(4, 2) TQ_GATE(4, 4) TQ_GATE(4, 8)
@@ -165,6 +175,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   __shared__ T buf[1 << CB];
   __shared__ int32_t lut[kS2MaxGates * kLut];            // group -> LDS address part
   __shared__ T cf[kS2MaxGates * kCf];                    // gate coefficients, k*N+n
+  __shared__ int32_t gmeta[kS2MaxGates * kGm];           // K, N, pass mask, kaddr, naddr
+  __shared__ S2Hot hot;
   const int tid = threadIdx.x;
   // ---- which op this workgroup works on (wave-uniform scan over <= 16 ranges)
   int j = 0;
@@ -190,6 +202,29 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       const S2Gate& gt = d->gate[g];
       if (t < gt.K * gt.N) cf[g * kCf + t] = reinterpret_cast<const T*>(op.G[g])[gt.gidx[t]];
     }
+  }
+  // ---- per-chunk tables -> LDS
+  for (int i = tid; i < kS2MaxSlots; i += NT) {
+    hot.ld_hm[i] = d->ld_hm[i];
+    hot.st_hm[i] = d->st_hm[i];
+    hot.ld_ha[i] = d->ld_ha[i];
+    hot.st_ha[i] = d->st_ha[i];
+  }
+  for (int i = tid; i < kS2MaxColBits; i += NT) {
+    hot.w_in[i] = d->w_in[i];
+    hot.w_out[i] = d->w_out[i];
+  }
+  // ---- gate fields -> LDS
+  for (int i = tid; i < ngates * kGm; i += NT) {
+    const S2Gate& gt = d->gate[i / kGm];
+    const int f = i % kGm;
+    int v = 0;
+    if (f == kGmK) v = gt.K;
+    else if (f == kGmN) v = gt.N;
+    else if (f == kGmPass) v = (int)gt.pass_mask;
+    else if (f < kGmNaddr) v = gt.kaddr[f - kGmKaddr];
+    else if (f < kGmNaddr + kS2MaxKN) v = gt.naddr[f - kGmNaddr];
+    gmeta[i] = v;
   }
   // ---- group tables -> LDS: LDS address part (positions << logC) ^ swizzle of group pp
   for (int g = 0; g < ngates; ++g) {
@@ -241,19 +276,19 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     else { TQ_SLOTS(1, BODY) }                                   \
   } while (0)
   auto prefetch = [&](int64_t ch) {
-    const int64_t base = chunk_base(ch, d->w_in);
-    TQ_BY_COUNT(rin, reg[r] = *lane_at(X + base + d->ld_hm[r], ldo));
+    const int64_t base = chunk_base(ch, hot.w_in);
+    TQ_BY_COUNT(rin, reg[r] = *lane_at(X + base + hot.ld_hm[r], ldo));
   };
   int64_t ch = lb;
   if (ch < nchunks) prefetch(ch);
   for (; ch < nchunks; ch += nb) {
-    TQ_BY_COUNT(rin, buf[lda ^ d->ld_ha[r]] = reg[r]);
+    TQ_BY_COUNT(rin, buf[lda ^ hot.ld_ha[r]] = reg[r]);
     __syncthreads();
     for (int g = 0; g < ngates; ++g) {
-      run_gate<T>(buf, cf + g * kCf, &d->gate[g], lut + g * kLut, logC);
+      run_gate<T>(buf, cf + g * kCf, gmeta + g * kGm, lut + g * kLut, logC);
       __syncthreads();
     }
-    const int64_t base = chunk_base(ch, d->w_out);
+    const int64_t base = chunk_base(ch, hot.w_out);
     // the next chunk's loads go out first (the wait for them at the top of the next iteration
     // then leaves this chunk's stores in flight); the tile leaves LDS in batches of 4 register
     // slots, each batch stored before the next is read (keeps the register budget)
@@ -263,11 +298,11 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       for (int r0 = 0; r0 < rout; r0 += 4) {
         T t[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ d->st_ha[r0 + q]];
+        for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ hot.st_ha[r0 + q]];
         if (st_lane) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            T* p = lane_at(Y + base + d->st_hm[r0 + q], sto);
+            T* p = lane_at(Y + base + hot.st_hm[r0 + q], sto);
             *p = use_beta ? scale_add(t[q], *p, beta) : t[q];
           }
         }
@@ -275,10 +310,10 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       }
     } else {
       T t[4];
-      TQ_BY_COUNT(rout, t[r] = buf[sta ^ d->st_ha[r]]);
+      TQ_BY_COUNT(rout, t[r] = buf[sta ^ hot.st_ha[r]]);
       if (st_lane) {
         TQ_BY_COUNT(rout, {
-          T* p = lane_at(Y + base + d->st_hm[r], sto);
+          T* p = lane_at(Y + base + hot.st_hm[r], sto);
           *p = use_beta ? scale_add(t[r], *p, beta) : t[r];
         });
       }
