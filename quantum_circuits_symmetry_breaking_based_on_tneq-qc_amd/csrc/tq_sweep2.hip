@@ -44,6 +44,8 @@ constexpr int kCf = kS2MaxKN * kS2MaxKN;     // coefficient slots per gate
 // must not queue behind the chunk's HBM stores (descriptor loads are vector loads)
 constexpr int kGmK = 0, kGmN = 1, kGmPass = 2, kGmKaddr = 3, kGmNaddr = kGmKaddr + kS2MaxK;
 constexpr int kGm = 16;
+constexpr int kDescWords2 = (int)(sizeof(S2Desc) / 8);
+static_assert(sizeof(S2Desc) % 8 == 0, "descriptor copy granularity");
 
 // per-chunk tables of the load / store phases, staged in LDS for the same reason
 struct S2Hot {
@@ -184,6 +186,13 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
   const S2Op& op = L.op[j];
   const S2Desc* __restrict__ d = op.desc;
+  // ---- the descriptor is staged in the (not yet used) tile buffer by one coalesced pass; the
+  // tables below are built from that copy (no chains of dependent scalar loads)
+  {
+    const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(d);
+    uint2* bd = reinterpret_cast<uint2*>(buf);
+    for (int i = tid; i < kDescWords2; i += NT) bd[i] = gd[i];
+  }
   const T* __restrict__ X = reinterpret_cast<const T*>(op.X);
   T* __restrict__ Y = reinterpret_cast<T*>(op.Y);
   const int lb = (int)blockIdx.x - op.block_begin, nb = op.nblocks;
@@ -195,28 +204,30 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   const int rin = (nin + NT - 1) / NT, rout = (nout + NT - 1) / NT;  // slots in use (powers of 2)
   const bool use_beta = op.use_beta;
   const double beta = op.beta;
+  __syncthreads();
+  const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
   // ---- gate coefficients -> LDS (one wave per gate)
   {
     const int g = tid >> 6, t = tid & 63;
     if (g < ngates) {
-      const S2Gate& gt = d->gate[g];
+      const S2Gate& gt = ds->gate[g];
       if (t < gt.K * gt.N) cf[g * kCf + t] = reinterpret_cast<const T*>(op.G[g])[gt.gidx[t]];
     }
   }
   // ---- per-chunk tables -> LDS
   for (int i = tid; i < kS2MaxSlots; i += NT) {
-    hot.ld_hm[i] = d->ld_hm[i];
-    hot.st_hm[i] = d->st_hm[i];
-    hot.ld_ha[i] = d->ld_ha[i];
-    hot.st_ha[i] = d->st_ha[i];
+    hot.ld_hm[i] = ds->ld_hm[i];
+    hot.st_hm[i] = ds->st_hm[i];
+    hot.ld_ha[i] = ds->ld_ha[i];
+    hot.st_ha[i] = ds->st_ha[i];
   }
   for (int i = tid; i < kS2MaxColBits; i += NT) {
-    hot.w_in[i] = d->w_in[i];
-    hot.w_out[i] = d->w_out[i];
+    hot.w_in[i] = ds->w_in[i];
+    hot.w_out[i] = ds->w_out[i];
   }
   // ---- gate fields -> LDS
   for (int i = tid; i < ngates * kGm; i += NT) {
-    const S2Gate& gt = d->gate[i / kGm];
+    const S2Gate& gt = ds->gate[i / kGm];
     const int f = i % kGm;
     int v = 0;
     if (f == kGmK) v = gt.K;
@@ -228,14 +239,14 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   }
   // ---- group tables -> LDS: LDS address part (positions << logC) ^ swizzle of group pp
   for (int g = 0; g < ngates; ++g) {
-    const uint32_t mask = d->gate[g].pass_mask;
+    const uint32_t mask = ds->gate[g].pass_mask;
     if (tid < (1 << __popc(mask))) {
       int base = 0, sw = 0;
       uint32_t m = mask;
       for (int t = 0; m; ++t) {
         const int lo = __builtin_ctz(m);
         m &= m - 1;
-        if ((tid >> t) & 1) { base |= 1 << lo; sw ^= d->vsw[lo]; }
+        if ((tid >> t) & 1) { base |= 1 << lo; sw ^= ds->vsw[lo]; }
       }
       lut[g * kLut + tid] = (base << logC) ^ (sw & cm);
     }
@@ -247,8 +258,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   {
     const int ti = tid & (nin - 1), to = tid & (nout - 1);
     for (int b = 0; b < LOG_NT; ++b) {
-      if (b < nld && ((ti >> b) & 1)) { ldm += d->ld_w[b]; lda ^= d->ld_a[b]; }
-      if (b < nst && ((to >> b) & 1)) { stm += d->st_w[b]; sta ^= d->st_a[b]; }
+      if (b < nld && ((ti >> b) & 1)) { ldm += ds->ld_w[b]; lda ^= ds->ld_a[b]; }
+      if (b < nst && ((to >> b) & 1)) { stm += ds->st_w[b]; sta ^= ds->st_a[b]; }
     }
   }
   const bool st_lane = tid < nout;
