@@ -706,7 +706,7 @@ class Compiler {
 
   // tile modes / working sets of a chain; false if it does not fit the sweep kernel's limits
   bool chain_shape(const Chain& c, const std::vector<int>& out_modes, ChainShape& sh) {
-    if ((int)c.gates.size() > kSweepMaxGates) return false;
+    if ((int)c.gates.size() > std::max(kSweepMaxGates, kS2MaxGates)) return false;
     std::set<int> contracted;
     for (auto& g : c.gates) {
       if (g.d.K * g.d.N > kSweepMaxKN) return false;
@@ -739,7 +739,8 @@ class Compiler {
     sh.wmax = std::max({sh.wmax, sh.tin_n, sh.tout_n});
     int64_t tab = 0;
     for (size_t j = 0; j < c.gates.size(); ++j) tab += count_of(sh.W[j]) * (c.gates[j].d.K + 1);
-    const bool old_ok = sh.wmax <= sweep_wmax((int)P_.esz) && tab <= kSweepTabMax;
+    const bool old_ok = (int)c.gates.size() <= kSweepMaxGates && sh.wmax <= sweep_wmax((int)P_.esz) &&
+                        tab <= kSweepTabMax;
     sh.s2 = s2_layout(c, sh, out_modes, nullptr);
     return old_ok || sh.s2;
   }
@@ -749,6 +750,13 @@ class Compiler {
     int l = 0;
     while ((int64_t(1) << l) < v) ++l;
     return l;
+  }
+  static int64_t s2_small_elems() {
+    static const int64_t v = [] {
+      const char* e = getenv("TQ_S2_SMALL");
+      return e ? (int64_t)atoll(e) : (int64_t(1) << 22);
+    }();
+    return v;
   }
   static int s2_min_chunks() {
     static const int v = [] {
@@ -787,7 +795,16 @@ class Compiler {
   bool s2_layout(const Chain& c, const ChainShape& sh, const std::vector<int>& out_modes,
                  S2Desc* out) {
     if (!s2_enabled() || c.gates.empty() || (int)c.gates.size() > kS2MaxGates) return false;
-    const int maxpos = s2_max_pos((int)P_.esz);
+    // tiles beyond 2^(chunk bits - 5) positions leave fewer than 32 columns per chunk and the
+    // gate passes 2- to 4-way LDS bank conflicts: only small (latency-bound) tensors use them,
+    // where the longer chains save launches
+    int maxpos = s2_max_pos((int)P_.esz);
+    {
+      int64_t nx = 1, ny = 1;
+      for (int m : c.X0.modes) nx *= ext_[m];
+      for (int m : out_modes) ny *= ext_[m];
+      if (std::max(nx, ny) > s2_small_elems()) maxpos = std::min(maxpos, s2_chunk_bits((int)P_.esz) - 5);
+    }
     auto nbits = [&](int m) { return ilog2(ext_[m]); };
     for (int m : c.X0.modes) if (nbits(m) < 0) return false;
     if (!c.X0.contiguous()) return false;
@@ -913,7 +930,7 @@ class Compiler {
     std::sort(st.begin(), st.end(), by_w);
     // swizzle vectors: the first 4 / 5 chunk bits of each enumeration (one 16- / 32-lane group)
     // must map to independent bank slots (mod 16 / mod 32)
-    int vsw[8];
+    int vsw[kS2MaxPos];
     for (int& v : vsw) v = -1;
     auto choose = [&](const std::vector<CBit>& e) {
       std::vector<int> vec;
@@ -936,7 +953,7 @@ class Compiler {
     };
     choose(ld);
     choose(st);
-    for (int p = 0; p < 8; ++p) d.vsw[p] = vsw[p] < 0 ? 0 : vsw[p];
+    for (int p = 0; p < kS2MaxPos; ++p) d.vsw[p] = vsw[p] < 0 ? 0 : vsw[p];
     auto code = [&](const CBit& b) {
       if (b.col >= 0) return 1 << b.col;
       return ((1 << b.pos) << kS2CodeP) | (d.vsw[b.pos] << kS2CodeS);
@@ -948,7 +965,8 @@ class Compiler {
     for (size_t t = 0; t < st.size(); ++t) { d.st_w[t] = st[t].w; d.st_code[t] = code(st[t]); }
     // LDS element address of a code: (p << logC) + (c ^ (s & (C-1))) -- XOR-linear in the code
     auto lds_addr = [&](int cd) {
-      const int p = (cd >> kS2CodeP) & 0xFF, cc = cd & ((1 << kS2CodeP) - 1), sv = (cd >> kS2CodeS) & 31;
+      const int p = (cd >> kS2CodeP) & ((1 << kS2MaxPos) - 1), cc = cd & ((1 << kS2CodeP) - 1),
+                sv = (cd >> kS2CodeS) & 31;
       return (p << d.logC) + (cc ^ (sv & ((1 << d.logC) - 1)));
     };
     for (int t = 0; t < d.nld; ++t) d.ld_a[t] = lds_addr(d.ld_code[t]);
@@ -965,7 +983,7 @@ class Compiler {
     }
     auto swz = [&](int bits) {
       int v = 0;
-      for (int p = 0; p < 8; ++p) if ((bits >> p) & 1) v ^= d.vsw[p];
+      for (int p = 0; p < kS2MaxPos; ++p) if ((bits >> p) & 1) v ^= d.vsw[p];
       return v;
     };
     const int cmask = (1 << d.logC) - 1;
@@ -988,7 +1006,7 @@ class Compiler {
       fprintf(stderr, " | st:");
       for (int t = 0; t < d.nst; ++t) fprintf(stderr, " %lld/%x", (long long)d.st_w[t], d.st_code[t]);
       fprintf(stderr, " | vsw:");
-      for (int p = 0; p < 8; ++p) fprintf(stderr, " %d", d.vsw[p]);
+      for (int p = 0; p < kS2MaxPos; ++p) fprintf(stderr, " %d", d.vsw[p]);
       fprintf(stderr, " | gates:");
       for (size_t j = 0; j < c.gates.size(); ++j)
         fprintf(stderr, " [K%d N%d pass%x]", d.gate[j].K, d.gate[j].N, d.gate[j].pass_mask);

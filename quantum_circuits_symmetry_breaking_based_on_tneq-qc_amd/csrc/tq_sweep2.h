@@ -11,7 +11,7 @@
 
 namespace tq {
 
-constexpr int kS2MaxGates = 8;
+constexpr int kS2MaxGates = 16;
 constexpr int kS2MaxKN = 8;            // N <= 8 per gate (coefficient slots: 8 x 8)
 constexpr int kS2MaxK = 4;             // K <= 4 per gate (exact-shape gate passes)
 constexpr int kS2MaxOps = 16;          // independent sweep ops batched into one launch
@@ -20,11 +20,12 @@ constexpr int kS2MaxChunkBits = 13;    // log2(chunk elements) for 8-byte elemen
 constexpr int kS2MaxColBits = 48;
 constexpr int kS2LogThreads = 9;       // 512 threads per workgroup
 constexpr int kS2MaxSlots = 16;        // chunk elements per thread (load / store register slots)
-inline int s2_max_pos(int esz) { return esz > 8 ? 7 : 8; }  // tile positions (index bits)
+constexpr int kS2MaxPos = 10;         // tile positions (index bits), at most
+inline int s2_max_pos(int esz) { return esz > 8 ? 9 : 10; }
 inline int s2_chunk_bits(int esz) { return esz > 8 ? 12 : 13; }
 
-// chunk-element code: column bits [0,13), position bits [13,21), swizzle [21,26); all XOR-combined
-constexpr int kS2CodeP = 13, kS2CodeS = 21;
+// chunk-element code: column bits [0,13), position bits [13,23), swizzle [23,28); all XOR-combined
+constexpr int kS2CodeP = 13, kS2CodeS = 23;
 
 struct S2Gate {
   int K = 0, N = 0;
@@ -52,7 +53,7 @@ struct S2Desc {
   int32_t ld_ha[kS2MaxSlots] = {}, st_ha[kS2MaxSlots] = {};
   int32_t ld_hc[kS2MaxSlots] = {}, st_hc[kS2MaxSlots] = {};
   int64_t w_in[kS2MaxColBits] = {}, w_out[kS2MaxColBits] = {};  // column-bit weights
-  int32_t vsw[8] = {};           // swizzle vector of each position
+  int32_t vsw[12] = {};          // swizzle vector of each position (kS2MaxPos used)
   S2Gate gate[kS2MaxGates];
 };
 

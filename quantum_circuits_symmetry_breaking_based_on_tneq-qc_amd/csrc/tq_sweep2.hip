@@ -38,8 +38,9 @@ namespace tq {
 namespace {
 
 constexpr int NT = 512, LOG_NT = 9;
-constexpr int kLut = 128;                    // per-gate group table entries (<= 7 pass positions)
-constexpr int kCf = kS2MaxKN * kS2MaxKN;     // coefficient slots per gate
+constexpr int kLut = 64;                     // per-gate group tables: 32 entries for the low 5 pass bits,
+                                             // 32 for the high ones (<= 9 pass positions)
+constexpr int kCf = kS2MaxK * kS2MaxKN;      // coefficient slots per gate
 // per-gate fields the gate passes read, staged in LDS: read in every pass of every chunk, they
 // must not queue behind the chunk's HBM stores (descriptor loads are vector loads)
 constexpr int kGmK = 0, kGmN = 1, kGmPass = 2, kGmKaddr = 3, kGmNaddr = kGmKaddr + kS2MaxK;
@@ -127,7 +128,8 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
       int gi = g0 + u * NT;
       ok[u] = gi < ngroups;
       gi = ok[u] ? gi : g0;
-      a0[u] = lut[gi >> logC] ^ (gi & cm);
+      const int gp = gi >> logC;
+      a0[u] = lut[gp & 31] ^ lut[32 + (gp >> 5)] ^ (gi & cm);
     }
     T x[U][K];
 #pragma unroll
@@ -206,13 +208,11 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   const double beta = op.beta;
   __syncthreads();
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
-  // ---- gate coefficients -> LDS (one wave per gate)
-  {
-    const int g = tid >> 6, t = tid & 63;
-    if (g < ngates) {
-      const S2Gate& gt = ds->gate[g];
-      if (t < gt.K * gt.N) cf[g * kCf + t] = reinterpret_cast<const T*>(op.G[g])[gt.gidx[t]];
-    }
+  // ---- gate coefficients -> LDS
+  for (int i = tid; i < ngates * kCf; i += NT) {
+    const int g = i / kCf, t = i % kCf;
+    const S2Gate& gt = ds->gate[g];
+    if (t < gt.K * gt.N) cf[i] = reinterpret_cast<const T*>(op.G[g])[gt.gidx[t]];
   }
   // ---- per-chunk tables -> LDS
   for (int i = tid; i < kS2MaxSlots; i += NT) {
@@ -237,19 +237,19 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     else if (f < kGmNaddr + kS2MaxKN) v = gt.naddr[f - kGmNaddr];
     gmeta[i] = v;
   }
-  // ---- group tables -> LDS: LDS address part (positions << logC) ^ swizzle of group pp
-  for (int g = 0; g < ngates; ++g) {
-    const uint32_t mask = ds->gate[g].pass_mask;
-    if (tid < (1 << __popc(mask))) {
-      int base = 0, sw = 0;
-      uint32_t m = mask;
-      for (int t = 0; m; ++t) {
-        const int lo = __builtin_ctz(m);
-        m &= m - 1;
-        if ((tid >> t) & 1) { base |= 1 << lo; sw ^= ds->vsw[lo]; }
-      }
-      lut[g * kLut + tid] = (base << logC) ^ (sw & cm);
+  // ---- group tables -> LDS: LDS address part (positions << logC) ^ swizzle of the pass bits of a
+  // group index, split into its low 5 and high bits (both parts are XOR-linear, so they combine by ^)
+  for (int i = tid; i < ngates * kLut; i += NT) {
+    const int g = i / kLut, j = i % kLut, half = j >> 5, v = j & 31;
+    uint32_t m = ds->gate[g].pass_mask;
+    int base = 0, sw = 0;
+    for (int t = 0; m; ++t) {
+      const int lo = __builtin_ctz(m);
+      m &= m - 1;
+      if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= ds->vsw[lo]; }
+      if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= ds->vsw[lo]; }
     }
+    lut[i] = (base << logC) ^ (sw & cm);
   }
   // ---- per-thread part of the load / store enumerations (low LOG_NT chunk bits); threads
   // beyond a small chunk duplicate element tid % n (same value to the same place)
