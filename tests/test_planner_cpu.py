@@ -90,10 +90,63 @@ def test_native_plan_c4_structure():
     gemm = [l for l in d if "GEMM" in l]
     assert "M=1024 N=1024" in gemm[0] and "[slice]" in gemm[0]
     assert p.query("n_ops_once") > 0.5 * p.query("n_kernels")   # most of the sweep is hoisted
-    # left / right sweeps are the two independent branches (two streams), the GEMM is the join
+    # left / right sweeps are the two independent branches, the GEMM is the join
     assert any(" b0 " in l for l in d) and any(" b1 " in l for l in d)
     assert " b2 " in gemm[0]
     assert p.query("flops") == pytest.approx(p.query("flops_once") + 8 * p.query("flops_slice"), rel=1e-6)
+
+
+def _schedule(d):
+    once, per = [], []
+    for l in d:
+        if l.startswith("# once"):
+            once.append([int(x) for x in l.split()[2:]])
+        elif l.startswith("# slice"):
+            per.append([int(x) for x in l.split()[2:]])
+    return once, per
+
+
+def test_launch_schedule_covers_every_op_once_and_batches_sweeps():
+    """Every op appears in exactly one launch of its set (hoisted / per slice), launches with more
+    than one op hold only independent SWEEP2 ops, and the C4 sweeps share launches."""
+    e, p = _plan(config_task("C4"))
+    d = p.describe().splitlines()
+    ops = [l for l in d if l.startswith("[once]") or l.startswith("[slice]")]
+    once, per = _schedule(d)
+    seen = sorted(j for g in once + per for j in g)
+    assert seen == list(range(len(ops)))
+    for g in once:
+        assert all(ops[j].startswith("[once]") for j in g)
+    for g in per:
+        assert all(ops[j].startswith("[slice]") for j in g)
+    for g in once + per:
+        if len(g) > 1:
+            assert len(g) <= 16 and all("SWEEP2" in ops[j] for j in g)
+    assert p.query("n_launch_once") == len(once) and p.query("n_launch_slice") == len(per)
+    assert p.query("n_sweep2") > 100 and len(once) < p.query("n_ops_once")
+    # the GEMM of a slice waits for both branch sweeps: it is alone in its launch, after them
+    gi = [k for k, g in enumerate(per) for j in g if "GEMM" in ops[j]]
+    assert len(gi) == 1 and len(per[gi[0]]) == 1 and gi[0] > 0
+
+
+def test_sweep_tiles_keep_32_columns_on_large_tensors():
+    """Tiles with more than 2^(13-5) positions (fewer than 32 columns per chunk) are reserved for
+    tensors of at most 2^22 elements (SWEEP2 layout rule, csrc/tq_plan.cpp s2_layout)."""
+    import re
+    e, p = _plan(config_task("C4"))
+    n_wide = 0
+    for l in p.describe().splitlines():
+        m = re.search(r"SWEEP2 gates=(\d+) tin=(\d+) tout=(\d+) cols=(\d+) C=(\d+)", l)
+        if not m:
+            continue
+        g, tin, tout, cols, C = map(int, m.groups())
+        assert 1 <= g <= 16
+        if max(tin, tout) > 256:
+            n_wide += 1
+            assert max(tin, tout) * cols <= 1 << 22
+        elif max(tin, tout) * cols > 1 << 22:
+            assert C >= 32 or cols < 32
+    assert n_wide > 0
 
 
 def test_plan_rejects_bad_paths():
