@@ -63,4 +63,42 @@ for n_q, S, G in [(4, 256, 1000), (8, 64, 1000)]:
     torch.cuda.synchronize()
     dt_ = time.perf_counter() - t0
     res[f"sample_{n_q}q_S{S}_G{G}"] = {"s": dt_, "samples_per_s": S / dt_, "grid_points_per_s": S * G * n_q / dt_}
+# §8(f) row 2: one training step of the symmetry-breaking loop shape (C5: 8-qubit 5-cell masked
+# ansatz, complex128 core-only contraction, fidelity loss against a target, backward through the
+# HIP expression = one more contraction per core, one Stiefel SGDG step)
+from tneq_qc_amd.circuits import ansatz_qctn
+from tneq_qc_amd.contractor import EinsumStrategy
+be = BackendFactory.create_backend("hip", device="cuda:0", dtype="complex128")
+bw = ansatz_qctn()
+q = bw.qctn
+eq, shapes = EinsumStrategy.build_core_only_expression(q)
+expr = EinsumStrategy.create_contract_expression(eq, shapes)
+tgt = expr(*[be.convert_to_tensor(bw.cores[c]) for c in q.cores]).detach().reshape(-1)
+rng = np.random.default_rng(3)
+params = [be.convert_to_tensor(bw.cores[c] + 0.1 * (rng.standard_normal(bw.cores[c].shape)
+                                                     + 1j * rng.standard_normal(bw.cores[c].shape)))
+          for c in q.cores]
+state = {}
+
+
+def train_step():
+    global params, state
+    ps = [p.detach().requires_grad_(True) for p in params]
+    out = expr(*ps).reshape(-1)
+    loss = 1.0 - torch.vdot(tgt, out).abs() ** 2 / (torch.vdot(tgt, tgt).real * torch.vdot(out, out).real)
+    grads = torch.autograd.grad(loss, ps)
+    params, state = be.optimizer_update(ps, list(grads), state, "sgdg", {"learning_rate": 0.01})
+    return loss
+
+
+for _ in range(3):
+    train_step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+steps = 20
+for _ in range(steps):
+    loss = train_step()
+torch.cuda.synchronize()
+dt_ = (time.perf_counter() - t0) / steps
+res["train_step_C5_ansatz"] = {"ms_per_step": dt_ * 1e3, "cores": len(q.cores), "loss": float(loss.detach())}
 print(json.dumps(res))
