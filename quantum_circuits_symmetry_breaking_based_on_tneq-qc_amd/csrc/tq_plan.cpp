@@ -1484,10 +1484,6 @@ void plan_release(Plan& P) {
   drop_graph(P);
   if (P.cap_stream) (void)hipStreamDestroy(P.cap_stream);
   P.cap_stream = nullptr;
-  if (P.side_stream) (void)hipStreamDestroy(P.side_stream);
-  P.side_stream = nullptr;
-  for (auto e : P.sync_events) (void)hipEventDestroy(e);
-  P.sync_events.clear();
   for (auto& ev : P.ev_used) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   for (auto& ev : P.ev_free) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   P.ev_used.clear();

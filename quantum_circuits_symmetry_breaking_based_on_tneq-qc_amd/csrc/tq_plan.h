@@ -140,8 +140,6 @@ struct Plan {
   std::vector<GraphEntry> graphs;
   uint64_t graph_clock = 0;
   hipStream_t cap_stream = nullptr;
-  hipStream_t side_stream = nullptr;        // (unused: independent ops share launches instead)
-  std::vector<hipEvent_t> sync_events;
   int64_t graph_builds = 0, graph_launches = 0;
 };
 
