@@ -37,8 +37,8 @@ struct Op {
   BufRef a, b, c;       // permute: a -> c ; gemm: c = a*b ; apply: c = a (x) b ; axpy: c += a
   bool writes_output = false;
   bool invariant = false;  // reads no sliced input: run once per execute call (hoisted)
-  int branch = 0;          // 0 / 1: the two independent subtrees of the final step (run on two
-                           // streams concurrently); 2: the join (final step), after both
+  int branch = 0;          // 0 / 1: the two independent subtrees of the final step (own arena
+                           // regions; their sweeps share launches); 2: the join (final step)
   // permute
   int perm = -1;        // index into Plan::perms
   // gemm
