@@ -9,16 +9,24 @@ sliced -> 8 slices.  One "step" = all 2^20 amplitudes: every rank contracts slic
 rank, rank+N, ... (left/right line sweeps + boundary MFMA GEMM, slice-invariant work hoisted)
 into a partial-amplitude buffer, then one RCCL all-reduce (SUM) over xGMI.  Total work is fixed
 as N grows ("scaling": "strong").  Inputs (cores, vectors) are resident in HBM before timing.
+`--config C2 / C3` time the other amplitude configs the same way (C3 = 64 slices, C2 = one
+amplitude, no slicing).
 
-Prints ONE JSON line on rank 0 with `roofline` (dominant kernel = the boundary GEMM, timed with
-HIP events on its stream inside the timed region) and, at N=1, `cpu_baseline` (the oracle's
-numpy pairwise executor on a bounded sample of the same network).
+Timing: the headline (`value`, `ms_per_step`) is the production launch path — every step replays
+the plan's captured hipGraph, no events inside.  The dominant kernel's duration (`roofline`) is
+then measured in a separate pass of the same K steps in which the plan launches eagerly with HIP
+events around every GEMM launch on its stream (the kernels are identical; rocprofv3's average
+for the same command is committed under profiles/).
+
+Prints ONE JSON line on rank 0 with `roofline` and, at N=1, `cpu_baseline` (the oracle's numpy
+pairwise executor on a bounded sample of the same network, in the same dtype).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -27,72 +35,111 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, f32-in MFMA
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-N_OPEN_CPU = 20                 # open outputs in the CPU-baseline sample (one slice: ~10-30 s of numpy)
+N_OPEN_CPU = 20                 # open outputs in the CPU-baseline sample (one slice: ~5-15 s of numpy)
 
 
-def _pmc_traffic(config: str):
-    """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_gemm.json")
+def _profile_json(name: str, config: str):
+    """A committed rocprofv3 PMC summary under profiles/ (or None)."""
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("config") == config:
-            return d.get("hbm_bytes_per_launch")
+            return d
     except Exception:
         pass
     return None
 
 
-def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
-    """Oracle (numpy, complex128 pairwise tensordot) on a bounded sample of the same workload:
-    the C4 network with the same path, cut and slicing and N_OPEN_CPU open outputs, timed over
-    whole slices until ~min_seconds of CPU work; amplitudes/sec = 2^N_OPEN_CPU / (8 * mean
-    t_slice) (the slices are identical sub-contractions, so the extrapolation is linear)."""
-    import numpy as np
-    from oracle.contract_ref import contract as ref_contract
-    from tneq_qc_amd.circuits import BrickWall, amplitude_task
-    import tneq_qc_amd.einsum as E
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
 
-    circ = BrickWall(53, 20, 0)
-    open_q = list(range(27 - N_OPEN_CPU // 2, 27 + N_OPEN_CPU // 2))
-    t = amplitude_task(circ, open_q, cut=27, n_slice=3)
-    net = t.network()
-    sl = [net.symbols.index(s) for s in t.sliced]
+
+def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
+    """Oracle (numpy pairwise transpose+matmul, complex64 — the GPU path's dtype) on a bounded
+    sample of the same workload: the config's network with the same path, cut and slicing and
+    N_OPEN_CPU open outputs, timed over whole slices until ~min_seconds of CPU work;
+    amplitudes/sec = 2^N_OPEN_CPU / (n_slices * mean t_slice) (the slices are identical
+    sub-contractions, so the extrapolation is linear)."""
+    import numpy as np
+    from oracle.contract_ref import contract as ref_contract, sliced_operands
+    from tneq_qc_amd.circuits import config_task
+
+    t = config_task(circ_cfg)
+    n_sl = 1
+    ext = {}
+    for term, op in zip(t.eq.split("->")[0].split(","), t.operands):
+        for ch, e in zip(term, op.shape):
+            ext[ch] = e
+    for s in t.sliced:
+        n_sl *= ext[s]
+    threads = None
     try:
         from threadpoolctl import threadpool_info
         threads = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
     except Exception:
-        threads = os.cpu_count() or 1
-    eq_terms = t.eq.split("->")[0].split(",")
-    terms = ["".join(ch for ch in term if ch not in t.sliced) for term in eq_terms]
-    eq = ",".join(terms) + "->" + t.eq.split("->")[1]
-    n_sl = 2 ** len(sl)
-    ext = [net.extents[m] for m in sl]
+        pass
+    ops64 = [o.astype(np.complex64) for o in t.operands]
     done, dt = 0, 0.0
     while done < n_sl and dt < min_seconds:   # whole slices until ~min_seconds of CPU work
-        idx, rem = {}, done
-        for s_, e_ in zip(reversed(t.sliced), reversed(ext)):
-            idx[s_] = rem % e_
-            rem //= e_
-        ops = []
-        for term, op in zip(eq_terms, t.operands):
-            ix = tuple(idx[ch] if ch in t.sliced else slice(None) for ch in term)
-            ops.append(np.ascontiguousarray(op[ix]))
+        eq, sops = sliced_operands(t.eq, ops64, t.sliced, done)
         t0 = time.perf_counter()
-        ref_contract(eq, *ops, path=t.path)
+        ref_contract(eq, *sops, path=t.path, exact=False)
         dt += time.perf_counter() - t0
         done += 1
-    n_amp = 2 ** len(open_q)
+    n_amp = t.n_amplitudes
     return {
         "value": n_amp / (n_sl * dt / done),
         "unit": "amplitudes/s",
-        "cores": threads,
+        "cores": threads or (os.cpu_count() or 1),
         "kind": "port",
-        "sample": (f"oracle = numpy pairwise transpose+matmul executor (complex128, BLAS threads="
-                   f"{threads}) on the C4 53q depth-20 network, same path/cut/slicing, "
-                   f"{len(open_q)} open outputs ({n_amp} amplitudes); {done} of {n_sl} slices timed "
-                   f"({dt:.2f} s), extrapolated linearly to all {n_sl}"),
+        "host_cpus": os.cpu_count(),
+        "host_cpus_affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+        "cpu_model": _cpu_model(),
+        "sample": (f"oracle = numpy pairwise transpose+matmul executor in complex64 (the GPU dtype; "
+                   f"BLAS threads={threads}) on the {circ_cfg} network, same path/cut/slicing, "
+                   f"{n_amp} amplitudes; {done} of {n_sl} slices timed ({dt:.2f} s), "
+                   f"extrapolated linearly to all {n_sl}"),
     }
+
+
+def permute_probe(dev, rank: int = 26, reps: int = 5):
+    """tq_permute on a rank-`rank` binary-leg complex64 tensor (2^rank elements) with a seeded
+    random permutation, through a one-op plan: HIP-event kernel time, algorithmic bytes
+    2 * numel * 8 (north_star: "rocprof HBM GB/s on the permute")."""
+    import numpy as np
+    import torch
+    from tneq_qc_amd import _lib
+    from tneq_qc_amd.einsum import get_symbol
+    from tneq_qc_amd.expression import HipContractExpression
+
+    rng = np.random.default_rng(26)
+    p = rng.permutation(rank)
+    s = "".join(get_symbol(i) for i in range(rank))
+    e = HipContractExpression(s + "->" + "".join(s[i] for i in p), (2,) * rank)
+    x = torch.randn((2,) * rank, dtype=torch.complex64, device=dev)
+    y = torch.empty((2,) * rank, dtype=torch.complex64, device=dev)
+    e(x, out=y)
+    plan = e.plan(torch.complex64)
+    plan.profile(_lib.TQ_OP_PERMUTE)
+    for _ in range(reps):
+        e(x, out=y)
+    torch.cuda.synchronize()
+    r = plan.profile_read(_lib.TQ_OP_PERMUTE)
+    plan.profile(None)
+    ok = bool(torch.equal(y.cpu(), x.cpu().permute(*p.tolist()).contiguous()))
+    gbs = r["bytes"] / (r["ms"] / 1e3) / 1e9
+    del x, y
+    return {"rank": rank, "numel": 2 ** rank, "dtype": "c64", "perm": [int(v) for v in p],
+            "avg_launch_ms": r["ms"] / r["launches"], "GBps": gbs, "frac": gbs / PEAK_HBM_GBS,
+            "bit_exact": ok}
 
 
 def main():
@@ -100,7 +147,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C4")
+    ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -135,28 +182,37 @@ def main():
     def step():
         job(*ops, out=out)
 
+    def timed(k: int) -> float:
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    plan.profile(_lib.TQ_OP_GEMM)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    gemm = plan.profile_read(_lib.TQ_OP_GEMM)
-    plan.profile(None)
+    # ---- headline: production path (hipGraph replay per step, no events)
+    dt = timed(args.steps)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    graphs = plan.query("graph_launches")
 
-    # one untimed profiled step for the HBM-bound kernels (evidence for DESIGN.md)
+    # ---- dominant kernel: the same K steps launched eagerly with HIP events around every GEMM
+    plan.profile(_lib.TQ_OP_GEMM)
+    dt_prof = timed(args.steps)
+    gemm = plan.profile_read(_lib.TQ_OP_GEMM)
+    plan.profile(None)
+
+    # ---- one profiled step for the HBM-bound kernels (evidence for DESIGN.md)
     plan.profile(-1)
     step()
     torch.cuda.synchronize()
@@ -166,11 +222,17 @@ def main():
     n_amp = task.n_amplitudes
     g3m = bool(_lib.lib().tq_library_query(b"gemm_3m") == 1)
     value = n_amp * args.steps / dt
-    avg_gemm_s = gemm["ms"] / 1e3 / max(1, gemm["launches"])
-    gemm_flops = gemm["flops"] / max(1, gemm["launches"])
-    achieved = gemm_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
+    nl = max(1, gemm["launches"])
+    avg_gemm_s = gemm["ms"] / 1e3 / nl
+    alg_flops = gemm["flops"] / nl                      # 8*M*N*K complex GEMM flops per launch
+    exe_flops = alg_flops * (0.75 if g3m else 1.0)      # MFMA work executed: 3M = 6*M*N*K, 4M = 8*M*N*K
+    achieved = exe_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
+    alg_rate = alg_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
+    pmc_t = _profile_json("pmc_gemm.json", args.config)
+    pmc_b = _profile_json("pmc_gemm_busy_r02.json", args.config)
     apply_ = kinds["APPLY"]
     sweep_ = kinds["SWEEP"]
+    perm_ = kinds["PERMUTE"]
     res = {
         "metric": "amplitudes/sec + achieved MFMA TFLOP/s, 53q depth-20 RQC",
         "value": value,
@@ -194,20 +256,29 @@ def main():
             "slices": n_slices,
             "parallelism": f"slices{world}",
         },
+        "timing": {
+            "headline": "hipGraph replay of the whole plan per step (production path), no events",
+            "graph_launches_timed": graphs,
+            "eager_profiled_ms_per_step": dt_prof / args.steps * 1e3,
+        },
         "roofline": {
             "bound": "mfma",
             "kernel": ("boundary GEMM (complex64, LDS-DMA fed v_mfma_f32_32x32x2_f32, "
-                       + ("Gauss 3M: 3 real f32 MFMA per complex MAC" if g3m else "4 real f32 MFMA per complex MAC") + ")"),
+                       + ("Gauss 3M: 3 real f32 MFMA GEMMs per complex GEMM" if g3m
+                          else "4 real f32 MFMA GEMMs per complex GEMM") + ")"),
             "achieved": achieved,
             "peak": PEAK_FP32_MFMA_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
-            "achieved_definition": "algorithmic complex-GEMM flops 8*M*N*K per launch / avg launch time",
-            "mfma_executed_tflops": achieved * (0.75 if g3m else 1.0),
-            "mfma_frac": achieved * (0.75 if g3m else 1.0) / PEAK_FP32_MFMA_TFLOPS,
-            "traffic": _pmc_traffic(args.config),
+            "achieved_definition": ("executed MFMA flops per launch (3M: 6*M*N*K, 4M: 8*M*N*K real) / "
+                                    "avg launch time (HIP events on the GEMM's stream, eager pass)"),
+            "algorithmic_tflops": alg_rate,
+            "algorithmic_definition": "complex-GEMM flops 8*M*N*K per launch / avg launch time",
+            "mfma_busy_pmc": (pmc_b or {}).get("mfma_busy_frac"),
+            "traffic": (pmc_t or {}).get("hbm_bytes_per_launch"),
             "avg_launch_ms": avg_gemm_s * 1e3,
-            "flops_per_launch": gemm_flops,
+            "flops_per_launch_algorithmic": alg_flops,
+            "flops_per_launch_executed": exe_flops,
             "launches_timed": gemm["launches"],
         },
         "hbm_kernels": {
@@ -216,7 +287,7 @@ def main():
             "sweep_GBps": (sweep_["bytes"] / (sweep_["ms"] / 1e3) / 1e9) if sweep_["ms"] else None,
             "sweep_ms_per_step": sweep_["ms"],
             "sweep_launches_per_step": sweep_["launches"],
-            "permute_ms_per_step": kinds["PERMUTE"]["ms"],
+            "permute_ms_per_step": perm_["ms"],
             "gemm_ms_per_step": kinds["GEMM"]["ms"],
             "peak_GBps": PEAK_HBM_GBS,
         },
@@ -224,9 +295,16 @@ def main():
             "compile_s": t_plan,
             "kernels_per_slice": plan.query("n_kernels"),
             "hoisted_kernels": plan.query("n_ops_once"),
+            "launches_once": plan.query("n_launch_once"),
+            "launches_per_slice": plan.query("n_launch_slice"),
             "arena_GiB": plan.query("arena_bytes") / 2 ** 30,
         },
     }
+    if rank == 0:
+        try:
+            res["permute"] = permute_probe(dev)
+        except Exception as e:  # the probe must never hide the headline
+            res["permute"] = {"error": repr(e)}
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(args.config)

@@ -34,6 +34,29 @@ def _exact(a: np.ndarray) -> np.ndarray:
     return a.astype(np.complex128 if np.iscomplexobj(a) else np.float64, copy=False)
 
 
+def sliced_operands(eq: str, arrays: Sequence[np.ndarray], sliced: Sequence[str], slice_id: int):
+    """Operands of slice `slice_id` of a sliced contraction: every symbol in `sliced` is fixed to
+    the digit of `slice_id` (row-major over `sliced`, last fastest — the enumeration of
+    tq_plan_execute) and removed from the equation.  Returns (equation, operands)."""
+    terms, rhs = parse_equation(eq)
+    ext = {}
+    for t, a in zip(terms, arrays):
+        for c, e in zip(t, np.shape(a)):
+            ext[c] = e
+    idx, rem = {}, int(slice_id)
+    for s in reversed(list(sliced)):
+        idx[s] = rem % ext[s]
+        rem //= ext[s]
+    if rem:
+        raise ValueError("slice id out of range")
+    ops = []
+    for t, a in zip(terms, arrays):
+        ix = tuple(idx[c] if c in idx else slice(None) for c in t)
+        ops.append(np.ascontiguousarray(np.asarray(a)[ix]))
+    new_terms = ["".join(c for c in t if c not in idx) for t in terms]
+    return ",".join(new_terms) + "->" + rhs, ops
+
+
 def _sum_out(t: str, a: np.ndarray, keep: set) -> Tuple[str, np.ndarray]:
     axes = tuple(i for i, c in enumerate(t) if c not in keep)
     if axes:
@@ -105,8 +128,10 @@ def greedy_path(terms: Sequence[str], shapes: Sequence[Sequence[int]], rhs: str)
     return path
 
 
-def contract(eq: str, *arrays: np.ndarray, path=None) -> np.ndarray:
-    """Evaluate an einsum equation (unicode symbols allowed) in exact arithmetic."""
+def contract(eq: str, *arrays: np.ndarray, path=None, exact: bool = True) -> np.ndarray:
+    """Evaluate an einsum equation (unicode symbols allowed) in exact arithmetic (complex128 /
+    float64), or with exact=False in the operands' own dtype (the CPU baseline's complex64 run:
+    same plan, same dtype as the GPU path)."""
     terms, rhs = parse_equation(eq)
     if len(terms) != len(arrays):
         raise ValueError(f"equation has {len(terms)} operands, got {len(arrays)}")
@@ -117,7 +142,8 @@ def contract(eq: str, *arrays: np.ndarray, path=None) -> np.ndarray:
         for c, e in zip(t, a.shape):
             if ext.setdefault(c, e) != e:
                 raise ValueError(f"symbol {c!r} has inconsistent extents")
-    live = {i: (t, _exact(np.asarray(a))) for i, (t, a) in enumerate(zip(terms, arrays))}
+    conv = _exact if exact else (lambda a: a)
+    live = {i: (t, conv(np.asarray(a))) for i, (t, a) in enumerate(zip(terms, arrays))}
     if path is None:
         path = greedy_path(terms, [a.shape for a in arrays], rhs)
     nid = len(terms)

@@ -128,7 +128,14 @@ int tq_contract_pair(int dtype, int rankA, const int64_t* shapeA, const int32_t*
                      size_t ws_bytes, void* stream) {
   TQ_GUARD_BEGIN
   tq::Plan P;
+  // a one-shot plan: launched eagerly (no graph capture, no capture stream), and every HIP
+  // resource it holds (events, graphs, owned memory) is released on every return path
+  struct Release {
+    tq::Plan& p;
+    ~Release() { tq::plan_release(p); }
+  } release{P};
   TQ_TRY(pair_plan(P, dtype, rankA, shapeA, modesA, rankB, shapeB, modesB, rankC, modesC));
+  P.use_graph = false;
   const size_t need = P.arena_bytes + P.table_bytes + 256;
   TQ_CHECK_ARG(ws_bytes >= need || (P.arena_bytes + P.table_bytes) == 0, "workspace too small");
   char* ws = (char*)workspace;

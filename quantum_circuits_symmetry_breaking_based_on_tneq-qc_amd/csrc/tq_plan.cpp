@@ -741,7 +741,10 @@ class Compiler {
     for (size_t j = 0; j < c.gates.size(); ++j) tab += count_of(sh.W[j]) * (c.gates[j].d.K + 1);
     const bool old_ok = (int)c.gates.size() <= kSweepMaxGates && sh.wmax <= sweep_wmax((int)P_.esz) &&
                         tab <= kSweepTabMax;
-    sh.s2 = s2_layout(c, sh, out_modes, nullptr);
+    {
+      S2Desc scratch;  // the full layout (every limit checked), so flush_chain cannot fail on it
+      sh.s2 = s2_layout(c, sh, out_modes, &scratch);
+    }
     return old_ok || sh.s2;
   }
 
@@ -961,8 +964,11 @@ class Compiler {
     d.nld = (int)ld.size();
     d.nst = (int)st.size();
     if (d.nld > 16 || d.nst > 16) return false;
+    // the kernel carries the lane part of a load / store offset (the low kS2LogThreads chunk
+    // bits) as a 32-bit byte offset: chains on high-order legs of huge tensors do not fit
     for (size_t t = 0; t < ld.size(); ++t) { d.ld_w[t] = ld[t].w; d.ld_code[t] = code(ld[t]); }
     for (size_t t = 0; t < st.size(); ++t) { d.st_w[t] = st[t].w; d.st_code[t] = code(st[t]); }
+    if (!s2_lane_offsets_fit(d.ld_w, d.nld, d.st_w, d.nst, (int64_t)P_.esz)) return false;
     // LDS element address of a code: (p << logC) + (c ^ (s & (C-1))) -- XOR-linear in the code
     auto lds_addr = [&](int cd) {
       const int p = (cd >> kS2CodeP) & ((1 << kS2MaxPos) - 1), cc = cd & ((1 << kS2CodeP) - 1),
@@ -1406,6 +1412,7 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
 }
 
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
+  TQ_HIP(hipGetDevice(&P.device));
   if (arena || tables) {
     P.d_arena = arena;
     P.d_tables = tables;
@@ -1504,6 +1511,15 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
   TQ_CHECK_ARG(s_step >= 1, "slice_step");
   TQ_CHECK_ARG(s_begin >= 0 && s_end <= P.n_slices, "slice range");
   TQ_CHECK_ARG(P.arena_bytes == 0 || P.d_arena, "plan not materialized");
+  {
+    // a plan's arena, tables and graphs live on one device; running it with another device
+    // current would hand that device foreign pointers
+    int cur = -1;
+    TQ_HIP(hipGetDevice(&cur));
+    TQ_CHECK_ARG(P.device < 0 || cur == P.device,
+                 "plan was materialized on device " + std::to_string(P.device) +
+                     " but device " + std::to_string(cur) + " is current");
+  }
   if (P.profile || !P.use_graph || graphs_disabled())
     return plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, stream);
   Plan::GraphKey key;

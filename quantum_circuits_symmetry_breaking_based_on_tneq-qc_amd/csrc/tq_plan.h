@@ -103,6 +103,7 @@ struct Plan {
   void* d_arena = nullptr;
   void* d_tables = nullptr;
   bool owns_device = false;
+  int device = -1;          // HIP device the arena / tables / graphs belong to (set at materialize)
   // optional per-op-kind timing with HIP events on the execution stream (bench evidence)
   unsigned profile = 0;  // bit k set: time ops of kind k
   struct Ev { hipEvent_t a, b; int kind; double flops, bytes; };

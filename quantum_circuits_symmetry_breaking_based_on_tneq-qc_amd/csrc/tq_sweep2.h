@@ -72,6 +72,17 @@ struct S2Launch {
   S2Op op[kS2MaxOps];
 };
 
+// The kernel addresses a lane's element as (uniform 64-bit base) + (32-bit byte offset), the
+// offset being the summed memory weights of the low kS2LogThreads load / store chunk bits: an
+// op whose lane offsets could reach 4 GiB must not be lowered to sweep2.
+inline bool s2_lane_offsets_fit(const int64_t* ld_w, int nld, const int64_t* st_w, int nst,
+                                int64_t esz) {
+  int64_t l = 0, s = 0;
+  for (int b = 0; b < kS2LogThreads && b < nld; ++b) l += ld_w[b];
+  for (int b = 0; b < kS2LogThreads && b < nst; ++b) s += st_w[b];
+  return (l > s ? l : s) * esz < (int64_t(1) << 32);
+}
+
 // blocks a sweep op gets when launched (chunks are strided over them)
 inline int s2_blocks(int64_t nchunks) { return (int)(nchunks < 512 ? nchunks : 512); }
 

@@ -141,8 +141,14 @@ class HipContractExpression:
     def info(self):
         return path_info(self.net, self.path, self.sliced)
 
-    def plan(self, dtype: torch.dtype, strides=None) -> NativePlan:
-        key = (dtype, None if strides is None else tuple(tuple(s) for s in strides))
+    def plan(self, dtype: torch.dtype, strides=None, device: Optional[int] = None) -> NativePlan:
+        """The native plan for (dtype, input strides, device).  A plan's arena, tables and graphs
+        live on the device that was current at its first execute; the library refuses to run it
+        with another device current, so plans are keyed by device.  One plan serves one stream
+        at a time (its arena is shared by its launches)."""
+        if device is None:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else -1
+        key = (dtype, None if strides is None else tuple(tuple(s) for s in strides), int(device))
         p = self._plans.get(key)
         if p is None:
             with self._lock:
@@ -205,15 +211,17 @@ class HipContractExpression:
         ts = [t if all(s >= 0 for s in t.stride()) else t.contiguous() for t in ts]
         strides = [t.stride() for t in ts]
         contiguous = all(t.is_contiguous() for t in ts)
-        plan = self.plan(dt, None if contiguous else strides)
+        plan = self.plan(dt, None if contiguous else strides, dev.index)
         if out is None:
             out = torch.empty(self.out_shape, dtype=dt, device=dev)
             accumulate = False
-        elif tuple(out.shape) != self.out_shape or out.dtype != dt or not out.is_contiguous():
-            raise ValueError("out tensor has the wrong shape/dtype or is not contiguous")
+        elif (tuple(out.shape) != self.out_shape or out.dtype != dt or not out.is_contiguous()
+              or out.device != dev):
+            raise ValueError("out tensor has the wrong shape/dtype/device or is not contiguous")
         begin, end, step = (0, plan.n_slices, 1) if slice_range is None else slice_range
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        plan.execute([t.data_ptr() for t in ts], out.data_ptr(), stream, begin, end, step, accumulate)
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            plan.execute([t.data_ptr() for t in ts], out.data_ptr(), stream, begin, end, step, accumulate)
         return out
 
 

@@ -112,7 +112,7 @@ def test_random_networks_with_batch_modes(dev, dtype):
         ref = ref_contract(eq, *ops)
         _, got = _run((eq, [o.shape for o in ops]), ops, dtype, dev, optimize="greedy")
         assert got.shape == ref.shape, eq
-        assert _err(got, ref) < TOL[dtype] * 10, (eq, trial)
+        assert _err(got, ref) < TOL[dtype], (eq, trial)
 
 
 def test_autograd_matches_torch(dev):

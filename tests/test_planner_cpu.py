@@ -167,3 +167,31 @@ def test_plan_create_errors_map_to_valueerror():
     net_bad = Network([[0, 1], [1, 2]], [0, 2], {0: 2, 1: 3, 2: 2})
     with pytest.raises(ValueError):          # a sliced mode that is an output mode
         NativePlan(net_bad, [(0, 1)], torch.complex64, None, [0])
+
+
+@pytest.mark.parametrize("n_legs,want_s2", [(24, True), (34, False)])
+def test_sweep2_lane_offsets_stay_32bit(n_legs, want_s2):
+    """SWEEP2 carries a lane's load/store offset (the low 9 chunk bits of its enumeration) as a
+    32-bit byte offset (csrc/tq_sweep2.hip lane_at).  A chain of 4 two-leg gates on the 8
+    highest-order legs of a 2^n_legs complex64 tensor puts tile bits of stride 2^(n-8)..2^(n-5)
+    among those low bits: at n = 34 they reach 2^32 bytes and the plan must not use SWEEP2
+    (it falls back to per-gate APPLY); at n = 24 it does."""
+    import torch
+    from tneq_qc_amd.einsum import get_symbol
+    from tneq_qc_amd.expression import HipContractExpression
+    legs = [get_symbol(i) for i in range(n_legs)]
+    terms = ["".join(legs)]
+    cur = list(legs)
+    nxt = n_legs
+    for g in range(4):
+        a, b = cur[2 * g], cur[2 * g + 1]
+        na, nb = get_symbol(nxt), get_symbol(nxt + 1)
+        nxt += 2
+        terms.append(a + b + na + nb)
+        cur[2 * g], cur[2 * g + 1] = na, nb
+    eq = ",".join(terms) + "->" + "".join(cur)
+    shapes = [(2,) * n_legs] + [(2, 2, 2, 2)] * 4
+    path = [(0, 1)] + [(5 + i, 2 + i) for i in range(3)]
+    e = HipContractExpression(eq, *shapes, optimize=path)
+    d = e.plan(torch.complex64).describe()
+    assert ("SWEEP2" in d) == want_s2, d
