@@ -185,14 +185,14 @@ class QCTN:
         save_file(d, str(file_path), metadata={str(k): str(v) for k, v in (metadata or {}).items()})
 
     def load_cores(self, file_path: Union[str, Path], strict: bool = True) -> Mapping[str, str]:
-        """qctn.py:928-964: loaded cores become auto-scaled TNTensors."""
+        """qctn.py:928-964: loaded cores become auto-scaled TNTensors (tensor / max|tensor|, scale =
+        max|tensor|).  Returns the metadata the reference returns: its `load_file` result is a plain
+        dict (never a (tensors, metadata) tuple, qctn.py:944-949), so that is always {}."""
         if self.backend is None:
             raise RuntimeError("Backend must be initialized before loading cores.")
-        from safetensors import safe_open
         from safetensors.numpy import load_file
         d = load_file(str(file_path))
-        with safe_open(str(file_path), framework="numpy") as f:
-            meta = f.metadata() or {}
+        meta = {}
         for name in self.cores:
             k, kr, ki = f"core_{name}", f"core_{name}_real", f"core_{name}_imag"
             if kr in d:

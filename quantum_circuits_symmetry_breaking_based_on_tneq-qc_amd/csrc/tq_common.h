@@ -53,8 +53,9 @@ inline bool dtype_complex(int dt) { return dt == TQ_C64 || dt == TQ_C128; }
 inline bool dtype_valid(int dt) { return dt >= TQ_F32 && dt <= TQ_C128; }
 
 // Storage element types for the kernels.  Complex values are interleaved (re, im).
-struct c64 { float re, im; };
-struct c128 { double re, im; };
+// Naturally aligned (8 B / 16 B) so that one element is one global / LDS access, not two.
+struct alignas(8) c64 { float re, im; };
+struct alignas(16) c128 { double re, im; };
 
 template <typename T> struct Traits;
 template <> struct Traits<float>  { using R = float;  static constexpr bool cplx = false; static constexpr int code = TQ_F32; };

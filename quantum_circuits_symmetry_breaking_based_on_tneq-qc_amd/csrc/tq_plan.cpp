@@ -417,7 +417,7 @@ class Compiler {
     op.bytes = 2.0 * n * P_.esz;
     std::ostringstream o;
     o << "step " << step << " PERMUTE " << why << " " << modes_str(X.modes) << "->" << modes_str(order)
-      << " n=" << n << (pp.use_generic ? " [generic]" : "") << (to_output ? " ->OUT" : "");
+      << " n=" << n << " [" << perm_plan_kind(pp) << "]" << (to_output ? " ->OUT" : "");
     op.note = o.str();
     P_.perms.push_back(std::move(pp));
     P_.ops.push_back(op);

@@ -123,7 +123,7 @@ def test_sample_matches_oracle_with_fixed_draws(dev, monkeypatch):
 
 def test_gradient_api_matches_torch_autograd(dev):
     import torch
-    from tneq_qc_amd.contractor.hip_strategy import build_sandwich
+    from tneq_qc_amd.contractor.greedy_symbolic import greedy_equation
     from tneq_qc_amd.core import QCTN
     g, qr, cores = _circuit(3, 2, 11)
     eng = _engine("complex128")
@@ -137,7 +137,8 @@ def test_gradient_api_matches_torch_autograd(dev):
     mx = [torch.from_numpy(m).to(dev) for m in mx_np]
     loss, grads = eng.contract_with_compiled_strategy_for_gradient(q, states, mx)
     # torch autograd on CPU over the same L·M·R network (R = conj of the cores)
-    eq, recipe = build_sandwich(q, {i: 2 for i in range(3)}, {i: 3 for i in range(3)})
+    eq, recipe = greedy_equation(q, {i: 2 for i in range(3)}, {i: (3, 2, 2) for i in range(3)},
+                                 {c: 4 for c in q.cores})
     cp = {c: torch.tensor(cores[c], requires_grad=True) for c in q.cores}
     ops_ = []
     for kind, key in recipe:

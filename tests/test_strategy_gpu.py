@@ -135,3 +135,80 @@ def test_training_step_gradients_through_hip(backend):
         l2.backward()
         for p, r in zip(params, cp):
             assert torch.allclose(p.grad.cpu(), r.grad, atol=1e-10)
+
+
+def test_right_qctn_matches_oracle_greedy(backend):
+    """right_qctn = a QCTN (greedy_strategy.py:764-822): the right cores are not conjugated and
+    their axes are read through the reference's dim map; compared with the oracle's QCTNRef branch."""
+    import torch
+    from oracle.greedy_ref import greedy_contract
+    from oracle.qctn_ref import QCTNRef, random_cores
+    from tneq_qc_amd.contractor import StrategyCompiler
+    from tneq_qc_amd.core import QCTN
+    g, qr, cores = _setup(4, 2, 11)
+    rcores = random_cores(QCTNRef(g), 12)
+    q, qright = QCTN(g), QCTN(g)
+    n = q.nqubits
+    rng = np.random.default_rng(4)
+    states = [np.array([0.6, 0.8j], complex) for _ in range(n)]
+    mx = [rng.standard_normal((3, 2, 2)) + 1j * rng.standard_normal((3, 2, 2)) for _ in range(n)]
+    ref = greedy_contract(qr, cores, states, mx, right_qctn=QCTNRef(g), right_cores=rcores)
+    fn, name, _ = StrategyCompiler("balanced").compile(
+        q, {"circuit_states_shapes": tuple(s.shape for s in states),
+            "measure_shapes": tuple(m.shape for m in mx), "measure_is_matrix": True}, backend,
+        right_qctn=qright)
+    assert name == "hip_tree"
+    T = lambda x: torch.from_numpy(x).to("cuda:0")
+    got = fn({c: T(cores[c]) for c in q.cores}, [T(s) for s in states], [T(m) for m in mx],
+             {c: T(rcores[c]) for c in qright.cores}).cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-12
+
+
+def test_safetensors_round_trip_through_hip_backend(backend, tmp_path):
+    """save_cores from device cores, from_pretrained back (auto-scaled TNTensors), and the loaded
+    network contracts to the same amplitudes (qctn.py:902-983)."""
+    import torch
+    from tneq_qc_amd.core import QCTN, TNTensor
+    from tneq_qc_amd.core.engine_siamese import EngineSiamese
+    g, qr, cores = _setup(3, 2, 21)
+    q = QCTN(g, backend=backend)
+    q.cores_weights = {c: torch.from_numpy(cores[c]).to("cuda:0") for c in q.cores}
+    f = tmp_path / "c.safetensors"
+    q.save_cores(f)
+    q2 = QCTN.from_pretrained(g, f, backend=backend)
+    assert all(isinstance(q2.cores_weights[c], TNTensor) for c in q2.cores)
+    eng = EngineSiamese(backend, "balanced")
+    states = [backend.convert_to_tensor(np.array([1.0, 0.0], complex)) for _ in range(3)]
+    P = backend.convert_to_tensor(np.array([[0, 0], [0, 1]], complex)[None].repeat(2, 0))
+    a = eng.calculate_full_probability(q, states, [P] * 3)
+    b = eng.calculate_full_probability(q2, states, [P] * 3)
+    b = b.tensor * b.scale if isinstance(b, TNTensor) else b
+    assert torch.allclose(a, b, atol=1e-13)
+
+
+@pytest.mark.parametrize("case", ["no_mx_on_1", "no_state_on_2"])
+def test_open_legs_match_oracle_greedy(backend, case):
+    """Qubits without an Mx or a state leave legs open in the reference's group sweep
+    (greedy_strategy.py:105-223); the HIP strategy returns the same tensor, same axis order."""
+    import torch
+    from oracle.greedy_ref import greedy_contract
+    from tneq_qc_amd.contractor import StrategyCompiler
+    from tneq_qc_amd.core import QCTN
+    g, qr, cores = _setup(3, 2, 31)
+    q = QCTN(g)
+    rng = np.random.default_rng(5)
+    states = [rng.standard_normal(2) + 0j for _ in range(3)]
+    mx = [rng.standard_normal((3, 2, 2)) + 1j * rng.standard_normal((3, 2, 2)) for _ in range(3)]
+    if case == "no_mx_on_1":
+        mx = {0: mx[0], 2: mx[2]}
+    else:
+        states = states[:2]
+    ref = greedy_contract(qr, cores, states, mx)
+    T = lambda x: torch.from_numpy(x).to("cuda:0")
+    st = [T(s) for s in states]
+    mt = {k: T(v) for k, v in mx.items()} if isinstance(mx, dict) else [T(m) for m in mx]
+    fn, name, _ = StrategyCompiler("balanced").compile(q, {}, backend)
+    got = fn({c: T(cores[c]) for c in q.cores}, st, mt).cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-12
