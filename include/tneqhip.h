@@ -31,6 +31,9 @@
  *                       _eval_hermitenorm_batch(_np) (tneq_qc/core/engine_siamese.py:59-254).
  *   tq_inverse_cdf_sample — the clamp / cumsum / normalise / search / interpolate block of
  *                       EngineSiamese.sample (tneq_qc/core/engine_siamese.py:854-905).
+ *   tq_sgdg_step       — SGDG.step, the Stiefel / Cayley optimizer of the symmetry-breaking
+ *                       training loop (tneq_qc/optim/stiefel_optimizer_complex.py:77-176,
+ *                       called at symmetry_breaking_quantum.py:216-230).
  */
 #ifndef TNEQHIP_H
 #define TNEQHIP_H
@@ -160,6 +163,23 @@ int tq_hermite_features(int dtype, int64_t n_points, int K, const double* x, con
 int tq_inverse_cdf_sample(int dtype, int64_t n_rows, int64_t grid_size, const void* density,
                           int64_t ld_density, const void* grid_x, const float* u, void* samples,
                           int64_t samples_stride, void* stream);
+
+/* One SGDG optimizer step (tneq_qc/optim/stiefel_optimizer_complex.py:77-176, SGDG.step, with
+ * gutils.py unit / qr_retraction / matrix_norm_one) for n parameters of one group, one workgroup
+ * per parameter.  Parameter i is a rows[i] x cols[i] contiguous matrix (the parameter reshaped
+ * to (prod of its leading half dims) x (rest), as SGDG.step views it) with a gradient of the
+ * same shape and a momentum buffer.  flags[i]: TQ_SGDG_STIEFEL selects the Cayley branch (needs
+ * rows <= cols <= 32; buffer cols x rows), otherwise the SGD branch with weight decay /
+ * momentum / dampening / nesterov (buffer rows x cols; the gradient is updated in place by
+ * the weight decay, as d_p.add_ does); TQ_SGDG_BUF_INIT = the buffer holds the previous
+ * momentum (else it is initialised as the reference does: zeros / a copy of d_p);
+ * TQ_SGDG_RETRACT = qr_retraction of the row-normalised parameter first (the reference draws
+ * this with random.randint(1, 101) == 1 on the host).  Arithmetic in the parameter's precision. */
+enum { TQ_SGDG_STIEFEL = 1, TQ_SGDG_BUF_INIT = 2, TQ_SGDG_RETRACT = 4 };
+int tq_sgdg_step(int dtype, int n, void* const* params, void* const* grads, void* const* bufs,
+                 const int32_t* rows, const int32_t* cols, const int32_t* flags, double lr,
+                 double momentum, double dampening, double weight_decay, int nesterov,
+                 void* stream);
 
 #ifdef __cplusplus
 }

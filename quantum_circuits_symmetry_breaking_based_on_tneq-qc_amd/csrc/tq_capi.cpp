@@ -4,6 +4,7 @@
 #include <new>
 
 #include "tq_common.h"
+#include "tq_optim.h"
 #include "tq_plan.h"
 
 namespace tq {
@@ -26,8 +27,13 @@ extern "C" int64_t tq_library_query(const char* key) {
   if (k == "gemm_3m") return tq::gemm_3m() ? 1 : 0;
   if (k == "graphs") return tq::graphs_enabled() ? 1 : 0;
   if (k == "sweep") return tq::sweeps_enabled_global() ? 1 : 0;
+
   return -1;
 }
+
+// development only (not in the public header): drains the sweep2 phase stamps of a library
+// built with -DTQ_S2_TIMING (9 x u64 per record); returns the record count (0 otherwise)
+extern "C" int tq_debug_sweep2_timing(unsigned long long* out, int n) { return tq::sweep2_timing(out, n); }
 
 struct tq_plan_s {
   tq::Plan plan;
@@ -274,6 +280,33 @@ int tq_plan_destroy(tq_plan p) {
   tq::plan_release(p->plan);
   delete p;
   return TQ_OK;
+}
+
+int tq_sgdg_step(int dtype, int n, void* const* params, void* const* grads, void* const* bufs,
+                 const int32_t* rows, const int32_t* cols, const int32_t* flags, double lr,
+                 double momentum, double dampening, double weight_decay, int nesterov,
+                 void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(tq::dtype_valid(dtype), "dtype");
+  TQ_CHECK_ARG(n >= 0, "n");
+  if (n == 0) return TQ_OK;
+  TQ_CHECK_ARG(params && grads && bufs && rows && cols && flags, "null argument");
+  for (int b = 0; b < n; b += tq::kSgdgMaxBatch) {
+    tq::SgdgLaunch L{};
+    L.n = std::min(n - b, tq::kSgdgMaxBatch);
+    L.nesterov = nesterov;
+    L.lr = lr;
+    L.momentum = momentum;
+    L.dampening = dampening;
+    L.weight_decay = weight_decay;
+    for (int i = 0; i < L.n; ++i) {
+      L.p[i] = tq::SgdgParam{params[b + i], grads[b + i], bufs[b + i], rows[b + i], cols[b + i],
+                             flags[b + i], 0};
+    }
+    TQ_TRY(tq::sgdg_launch(dtype, L, (hipStream_t)stream));
+  }
+  return TQ_OK;
+  TQ_GUARD_END
 }
 
 }  // extern "C"

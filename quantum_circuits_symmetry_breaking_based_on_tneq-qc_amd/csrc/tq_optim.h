@@ -1,0 +1,34 @@
+// One SGDG step over a group of parameters in one launch (tq_optim.hip).
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace tq {
+
+constexpr int kSgdgStiefel = 1;   // Stiefel (Cayley) branch: rows <= cols and stiefel=True
+constexpr int kSgdgBufInit = 2;   // momentum buffer already holds a previous value
+constexpr int kSgdgRetract = 4;   // qr_retraction of the row-normalised parameter first
+constexpr int kSgdgMaxDim = 32;   // rows, cols <= 32 on the Stiefel branch (LDS-resident matrices)
+constexpr int kSgdgMaxBatch = 48; // parameters per launch (the descriptors travel as kernel arguments)
+
+struct SgdgParam {
+  void* param;       // rows x cols, contiguous (the parameter viewed as in SGDG.step)
+  void* grad;        // same shape; written back (weight decay) on the SGD branch
+  void* buf;         // momentum buffer: cols x rows (Stiefel) or rows x cols (SGD)
+  int rows, cols;
+  int flags;
+  int pad;
+};
+
+struct SgdgLaunch {
+  int n;
+  int nesterov;
+  double lr, momentum, dampening, weight_decay;
+  SgdgParam p[kSgdgMaxBatch];
+};
+
+// one workgroup per parameter; n <= kSgdgMaxBatch
+int sgdg_launch(int dtype, const SgdgLaunch& L, hipStream_t stream);
+
+}  // namespace tq

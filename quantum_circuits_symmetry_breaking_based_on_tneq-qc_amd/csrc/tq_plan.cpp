@@ -889,7 +889,10 @@ class Compiler {
         for (size_t t = 0; t < np.size(); ++t) if ((n >> t) & 1) v |= 1 << np[t];
         ndep[j].push_back(v);
       }
-      for (int t = 0; t < G.K * G.N; ++t) G.gidx[t] = g.d.gtab.empty() ? t : g.d.gtab[t];
+      for (int t = 0; t < G.K * G.N; ++t) {
+        G.gidx[t] = g.d.gtab.empty() ? t : g.d.gtab[t];
+        if (G.gidx[t] >= kS2GateRaw) return false;   // the kernel stages kS2GateRaw elements per gate
+      }
     }
     // the final working set must be the output tile
     {
@@ -1700,7 +1703,14 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[op.stab]);
           o.X = ptr(op.a);
           o.Y = ptr(op.c);
-          for (size_t g = 0; g < op.sgates.size(); ++g) o.G[g] = ptr(op.sgates[g].g);
+          const S2Desc* hd = reinterpret_cast<const S2Desc*>(P.stabs[op.stab].data());
+          for (size_t g = 0; g < op.sgates.size(); ++g) {
+            o.G[g] = ptr(op.sgates[g].g);
+            int mx = 0;
+            for (int t = 0; t < hd->gate[g].K * hd->gate[g].N; ++t) mx = std::max(mx, hd->gate[g].gidx[t] + 1);
+            if (mx > kS2GateRaw) { set_error("internal: sweep2 gate tensor too large"); return TQ_ERR_INVALID; }
+            o.gnum[g] = (uint8_t)mx;
+          }
           o.block_begin = blocks;
           o.nblocks = s2_blocks(op.s2_nchunks);
           blocks += o.nblocks;

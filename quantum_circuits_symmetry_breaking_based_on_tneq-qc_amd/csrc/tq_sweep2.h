@@ -15,6 +15,7 @@ constexpr int kS2MaxGates = 16;
 constexpr int kS2MaxKN = 8;            // N <= 8 per gate (coefficient slots: 8 x 8)
 constexpr int kS2MaxK = 4;             // K <= 4 per gate (exact-shape gate passes)
 constexpr int kS2MaxOps = 16;          // independent sweep ops batched into one launch
+constexpr int kS2GateRaw = 64;         // gate-tensor elements staged per gate
 constexpr int kS2ChunkBytes = 65536;   // LDS tile per workgroup
 constexpr int kS2MaxChunkBits = 13;    // log2(chunk elements) for 8-byte elements
 constexpr int kS2MaxColBits = 48;
@@ -62,6 +63,9 @@ struct S2Op {
   const void* X = nullptr;
   void* Y = nullptr;
   const void* G[kS2MaxGates] = {};
+  // elements of G[g] the gate reads (max gidx + 1, <= kS2GateRaw): staged by the kernel together
+  // with the descriptor, so the coefficient fetch is not a second dependent global round trip
+  uint8_t gnum[kS2MaxGates] = {};
   int block_begin = 0, nblocks = 0;
   double beta = 0.0;
   int use_beta = 0, pad = 0;
@@ -87,5 +91,6 @@ inline bool s2_lane_offsets_fit(const int64_t* ld_w, int nld, const int64_t* st_
 inline int s2_blocks(int64_t nchunks) { return (int)(nchunks < 512 ? nchunks : 512); }
 
 int sweep2_launch(int dtype, const S2Launch& L, hipStream_t stream);
+int sweep2_timing(unsigned long long* out, int n);   // development instrumentation
 
 }  // namespace tq

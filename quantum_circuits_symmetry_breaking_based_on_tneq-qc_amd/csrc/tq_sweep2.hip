@@ -56,6 +56,17 @@ struct S2Hot {
 };
 static_assert(kGmNaddr + kS2MaxKN <= kGm, "gate meta layout");
 
+#ifdef TQ_S2_TIMING
+// development instrumentation (built only with -DTQ_S2_TIMING): workgroup 0 of every op records
+// wall-clock stamps (100 MHz) at its phase boundaries
+constexpr int kTsMax = 4096, kTsPh = 9;
+__device__ unsigned long long g_s2_ts[kTsMax][kTsPh];
+__device__ unsigned int g_s2_seq;
+#define TQ_TS(ph) do { if (ts_rec && threadIdx.x == 0) g_s2_ts[ts_idx][ph] = wall_clock64(); } while (0)
+#else
+#define TQ_TS(ph) do {} while (0)
+#endif
+
 template <typename T>
 __device__ __forceinline__ T scale_add(T v, T y, double beta) {
   if constexpr (sizeof(typename Traits<T>::R) == 4) return v + y * (float)beta;
@@ -188,12 +199,29 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
   const S2Op& op = L.op[j];
   const S2Desc* __restrict__ d = op.desc;
+#ifdef TQ_S2_TIMING
+  const bool ts_rec = (int)blockIdx.x == op.block_begin;
+  __shared__ unsigned int ts_slot;
+  if (ts_rec && threadIdx.x == 0) ts_slot = atomicAdd(&g_s2_seq, 1u) % kTsMax;
+  __syncthreads();
+  const unsigned ts_idx = ts_slot;
+  TQ_TS(0);
+#endif
   // ---- the descriptor is staged in the (not yet used) tile buffer by one coalesced pass; the
   // tables below are built from that copy (no chains of dependent scalar loads)
+  // the gate tensors' raw elements go to the tile buffer behind the descriptor in the same pass
+  // (pointers and element counts are kernel arguments)
+  constexpr int kGrawOff = ((int)sizeof(S2Desc) + 255) / 256 * 256 / (int)sizeof(T);
+  static_assert(kGrawOff + kS2MaxGates * kS2GateRaw <= (1 << CB), "descriptor + raw gates fit the tile");
+  T* graw = buf + kGrawOff;
   {
     const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(d);
     uint2* bd = reinterpret_cast<uint2*>(buf);
     for (int i = tid; i < kDescWords2; i += NT) bd[i] = gd[i];
+    for (int i = tid; i < kS2MaxGates * kS2GateRaw; i += NT) {
+      const int g = i / kS2GateRaw, e = i % kS2GateRaw;
+      if (e < (int)op.gnum[g]) graw[i] = reinterpret_cast<const T*>(op.G[g])[e];
+    }
   }
   const T* __restrict__ X = reinterpret_cast<const T*>(op.X);
   T* __restrict__ Y = reinterpret_cast<T*>(op.Y);
@@ -207,12 +235,13 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   const bool use_beta = op.use_beta;
   const double beta = op.beta;
   __syncthreads();
+  TQ_TS(1);
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
   // ---- gate coefficients -> LDS
   for (int i = tid; i < ngates * kCf; i += NT) {
     const int g = i / kCf, t = i % kCf;
     const S2Gate& gt = ds->gate[g];
-    if (t < gt.K * gt.N) cf[i] = reinterpret_cast<const T*>(op.G[g])[gt.gidx[t]];
+    if (t < gt.K * gt.N) cf[i] = graw[g * kS2GateRaw + gt.gidx[t]];
   }
   // ---- per-chunk tables -> LDS
   for (int i = tid; i < kS2MaxSlots; i += NT) {
@@ -266,6 +295,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   // uniform part (chunk + register slot) in scalar registers, lane part as a 32-bit byte offset
   const uint32_t ldo = (uint32_t)(ldm * (int64_t)sizeof(T)), sto = (uint32_t)(stm * (int64_t)sizeof(T));
   __syncthreads();
+  TQ_TS(2);
   auto chunk_base = [&](int64_t ch, const int64_t* w) {
     int64_t o = 0;
     for (int b = logC; b < colbits; ++b)
@@ -290,21 +320,41 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     const int64_t base = chunk_base(ch, hot.w_in);
     TQ_BY_COUNT(rin, reg[r] = *lane_at(X + base + hot.ld_hm[r], ldo));
   };
+  // Chunk pipeline.  On this ISA one counter (vmcnt) covers loads and stores, and a wait for a
+  // load issued before some stores waits for those stores too (they may complete out of order),
+  // so the order below keeps every wait where nothing else is pending:
+  //   next chunk's loads -> gate passes -> wait(all) -> store this chunk -> tile <- next chunk
+  // the stores of a chunk then drain under the next chunk's gate passes and the loads of the
+  // chunk after it, instead of being waited for before that chunk can enter the tile.
   int64_t ch = lb;
-  if (ch < nchunks) prefetch(ch);
-  for (; ch < nchunks; ch += nb) {
+  if (ch < nchunks) {
+    prefetch(ch);
     TQ_BY_COUNT(rin, buf[lda ^ hot.ld_ha[r]] = reg[r]);
-    __syncthreads();
+  }
+  __syncthreads();
+  TQ_TS(3);
+#ifdef TQ_S2_TIMING
+  const unsigned long long clk0 = clock64();
+  unsigned long long clk_gates = 0;
+#endif
+  for (; ch < nchunks; ch += nb) {
+    const int64_t nxt = ch + nb;
+    const bool more = nxt < nchunks;
+    if (more) prefetch(nxt);
     for (int g = 0; g < ngates; ++g) {
       run_gate<T>(buf, cf + g * kCf, gmeta + g * kGm, lut + g * kLut, logC);
       __syncthreads();
     }
+    if (ch == lb) TQ_TS(4);
+#ifdef TQ_S2_TIMING
+    if (ch == lb) clk_gates = clock64() - clk0;
+#endif
+    // vmcnt(0) (expcnt / lgkmcnt unconstrained): the next chunk is in registers, the previous
+    // chunk's stores are done
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     const int64_t base = chunk_base(ch, hot.w_out);
-    // the next chunk's loads go out first (the wait for them at the top of the next iteration
-    // then leaves this chunk's stores in flight); the tile leaves LDS in batches of 4 register
-    // slots, each batch stored before the next is read (keeps the register budget)
-    const int64_t nxt = ch + nb;
-    if (nxt < nchunks) prefetch(nxt);
+    // the tile leaves LDS in batches of 4 register slots, each batch stored before the next is
+    // read (keeps the register budget)
     if (rout >= 4) {
       for (int r0 = 0; r0 < rout; r0 += 4) {
         T t[4];
@@ -329,8 +379,17 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
         });
       }
     }
-    __syncthreads();  // the tile is rewritten by the next chunk
+    __syncthreads();  // every wave has read the tile
+    if (ch == lb) TQ_TS(5);
+    if (more) TQ_BY_COUNT(rin, buf[lda ^ hot.ld_ha[r]] = reg[r]);
+    __syncthreads();
   }
+#ifdef TQ_S2_TIMING
+  __builtin_amdgcn_s_waitcnt(0);
+  TQ_TS(6);
+  if (ts_rec && threadIdx.x == 0) g_s2_ts[ts_idx][7] = ((unsigned long long)op.nblocks << 32) | (unsigned)nchunks;
+  if (ts_rec && threadIdx.x == 0) g_s2_ts[ts_idx][8] = clk_gates;
+#endif
 #undef TQ_BY_COUNT
 #undef TQ_SLOTS
 }
@@ -347,6 +406,24 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
 }
 
 }  // namespace
+
+// copies up to n records of 8 stamps (see g_s2_ts) and resets the sequence; 0 without the
+// instrumentation
+int sweep2_timing(unsigned long long* out, int n) {
+#ifdef TQ_S2_TIMING
+  unsigned seq = 0;
+  if (hipMemcpyFromSymbol(&seq, HIP_SYMBOL(g_s2_seq), sizeof(seq)) != hipSuccess) return -1;
+  const int cnt = (int)std::min<unsigned>(seq, (unsigned)std::min(n, kTsMax));
+  if (cnt > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s2_ts), sizeof(unsigned long long) * kTsPh * cnt) != hipSuccess)
+    return -1;
+  const unsigned zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_s2_seq), &zero, sizeof(zero)) != hipSuccess) return -1;
+  return cnt;
+#else
+  (void)out; (void)n;
+  return 0;
+#endif
+}
 
 int sweep2_launch(int dtype, const S2Launch& L, hipStream_t stream) {
   if (L.nops < 1 || L.nops > kS2MaxOps) {

@@ -1,0 +1,95 @@
+"""SGDG on the HIP kernel (tq_sgdg_step via tneq_qc_amd.optim.SGDG) vs the oracle's restatement
+of stiefel_optimizer_complex.py:77-176, several steps with momentum, for the workload's 4x4
+complex cores (Stiefel / Cayley branch, incl. the random qr_retraction draw) and a rows > cols
+parameter (SGD branch with weight decay / nesterov).  Same Python `random` seed on both sides.
+Tolerances: complex128 / float64 1e-12, complex64 / float32 1e-5 (relative to max |p|)."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"complex128": 1e-12, "float64": 1e-12, "complex64": 1e-5, "float32": 1e-5}
+
+
+def _params(rng, dtype, cplx):
+    shapes = [(2, 2, 2, 2)] * 5 + [(2, 2, 2)] + [(4, 2)]
+    out = []
+    for s in shapes:
+        a = rng.standard_normal(s)
+        if cplx:
+            a = a + 1j * rng.standard_normal(s)
+        out.append(a.astype(dtype))
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["complex128", "complex64", "float64", "float32"])
+def test_sgdg_steps_match_oracle(dev, dtype):
+    import torch
+    from oracle.optim_ref import sgdg_step
+    from tneq_qc_amd.optim import SGDG
+    cplx = dtype.startswith("complex")
+    rng = np.random.default_rng(7)
+    ref = _params(rng, np.dtype(dtype), cplx)
+    params = [torch.nn.Parameter(torch.from_numpy(p.copy()).to(dev)) for p in ref]
+    hp = dict(lr=0.05, momentum=0.9, weight_decay=0.01, nesterov=False, stiefel=True)
+    opt = SGDG(params, **hp)
+    state = {}
+    seeds = [next(s for s in range(10000) if (random.seed(s), random.randint(1, 101))[1] == 1), 5, 6]
+    for step, seed in enumerate(seeds):
+        grads = [(rng.standard_normal(p.shape) + (1j * rng.standard_normal(p.shape) if cplx else 0)).astype(dtype)
+                 for p in ref]
+        for p, g in zip(params, grads):
+            p.grad = torch.from_numpy(g.copy()).to(dev)
+        random.seed(seed)
+        opt.step()
+        random.seed(seed)
+        sgdg_step(ref, [g.copy() for g in grads], state, **hp)
+        torch.cuda.synchronize()
+        for i, (p, r) in enumerate(zip(params, ref)):
+            got = p.detach().cpu().numpy()
+            err = np.abs(got - r).max() / max(np.abs(r).max(), 1e-30)
+            assert err < TOL[dtype], (step, i, err)
+            if "momentum_buffer" in state.get(i, {}):
+                b = opt.state[p]["momentum_buffer"].cpu().numpy()
+                rb = state[i]["momentum_buffer"]
+                assert np.abs(b - rb).max() / max(np.abs(rb).max(), 1e-30) < TOL[dtype] * 10, (step, i)
+
+
+def test_sgdg_workload_loop_keeps_cores_unitary_and_fits(dev):
+    """A few iterations of the symmetry-breaking fit (symmetry_breaking_quantum.py:203-230):
+    fidelity loss through the HIP expression, backward, HIP SGDG step; cores stay unitary and
+    the loss decreases."""
+    import torch
+    from tneq_qc_amd.circuits import BrickWall
+    from tneq_qc_amd.contractor import EinsumStrategy
+    from tneq_qc_amd.optim import SGDG
+    bw = BrickWall(4, 4, 3)
+    q = bw.qctn
+    eq, shapes = EinsumStrategy.build_core_only_expression(q)
+    expr = EinsumStrategy.create_contract_expression(eq, shapes)
+    tgt = expr(*[torch.from_numpy(bw.cores[c]).to(dev) for c in q.cores]).detach().reshape(-1)
+    rng = np.random.default_rng(0)
+    init = []
+    for c in q.cores:
+        a, r = np.linalg.qr(rng.standard_normal((4, 4)) + 1j * rng.standard_normal((4, 4)))
+        init.append((a * (np.diag(r) / np.abs(np.diag(r)))[None, :]).reshape(2, 2, 2, 2))
+    params = [torch.nn.Parameter(torch.from_numpy(a).to(dev)) for a in init]
+    opt = SGDG(params, lr=1e-2, stiefel=True, momentum=0.9)
+    losses = []
+    random.seed(0)
+    for _ in range(30):
+        opt.zero_grad()
+        out = expr(*params).reshape(-1)
+        num = torch.vdot(tgt, out).abs() ** 2
+        den = (torch.vdot(tgt, tgt).real * torch.vdot(out, out).real).clamp_min(1e-12)
+        loss = 1.0 - num / den
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0]
+    eye = torch.eye(4, dtype=torch.complex128, device=dev)
+    for p in params:
+        u = p.detach().reshape(4, 4)
+        assert torch.allclose(u @ u.conj().T, eye, atol=1e-10)
