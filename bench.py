@@ -24,6 +24,7 @@ pairwise executor on a bounded sample of the same network, in the same dtype).
 from __future__ import annotations
 
 import argparse
+import math
 import json
 import os
 import platform
@@ -142,6 +143,41 @@ def permute_probe(dev, rank: int = 26, reps: int = 5):
             "bit_exact": ok}
 
 
+def c5_train(dev, with_cpu: bool = True, steps: int = 5, warmup: int = 2):
+    """Secondary line (BASELINE.json configs[4], C5): the symmetry-breaking training step —
+    8 pruning candidates x (core-only forward, fidelity loss, reverse-mode backward, SGDG) in
+    complex128 — next to the same step on the host CPU (scripts/c5_bench.py)."""
+    import importlib.util
+    import random
+    import torch
+    spec = importlib.util.spec_from_file_location("c5_bench", os.path.join(ROOT, "scripts", "c5_bench.py"))
+    cb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cb)
+    random.seed(0)
+    target, cands = cb.setup(dev)
+    for _ in range(warmup):
+        cb.gpu_step(target, cands)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cb.gpu_step(target, cands)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    r = {"metric": "candidate training steps/s (forward + backward + SGDG), C5 ansatz, 8 candidates",
+         "value": len(cands) / dt, "unit": "candidate-steps/s", "ms_per_step": dt * 1e3, "steps": steps,
+         "dtype": "c128", "cores_per_candidate": len(cands[0][1]),
+         "amplitudes_per_forward": int(math.prod(cands[0][0].out_shape)),
+         "bound": "latency (2^16-element tensors; ~100 dependent pairwise launches per candidate-step)"}
+    if with_cpu:
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        secs, n = cb.cpu_step_sample(target.cpu().numpy(), cands, 1)
+        r["cpu_baseline"] = {"value": n / secs, "unit": "candidate-steps/s", "cores": torch.get_num_threads(),
+                             "kind": "port", "cpu_model": _cpu_model(),
+                             "sample": f"{n} candidate-steps: torch CPU pairwise tensordot along the same "
+                                       "path + autograd + the oracle's SGDG restatement, complex128"}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,6 +185,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 training-step line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,6 +347,11 @@ def main():
             res["cpu_baseline"] = cpu_baseline(args.config)
         except Exception as e:  # the baseline must never hide the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
+    if world == 1 and rank == 0 and not args.no_c5:
+        try:
+            res["c5_train"] = c5_train(dev, with_cpu=not args.no_cpu_baseline)
+        except Exception as e:  # the secondary line must never hide the headline
+            res["c5_train"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

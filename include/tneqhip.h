@@ -121,6 +121,9 @@ int tq_plan_create(tq_plan* plan, int dtype, int n_inputs, const int32_t* in_ran
  * (slice-invariant part, hoisted: run once per execute), "flops_slice" / "bytes_slice"
  * (per slice), "n_kernels", "n_ops_once", "n_gemm", "n_apply", "n_permute".  -1 if unknown. */
 int64_t tq_plan_query(tq_plan plan, const char* key);
+/* Plan option: "graph" = 1 (default) replays the execute's launches from a captured hipGraph,
+ * 0 launches them eagerly on the stream (use when the caller captures the stream itself). */
+int tq_plan_set(tq_plan plan, const char* key, int64_t value);
 /* human-readable per-step description into buf (for debugging / DESIGN evidence) */
 int tq_plan_describe(tq_plan plan, char* buf, size_t n);
 

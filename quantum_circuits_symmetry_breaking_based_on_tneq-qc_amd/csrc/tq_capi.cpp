@@ -175,6 +175,20 @@ int tq_plan_create(tq_plan* out, int dtype, int n_inputs, const int32_t* in_rank
   TQ_GUARD_END
 }
 
+int tq_plan_set(tq_plan p, const char* key, int64_t value) {
+  if (!p || !key) {
+    tq::set_error("tq_plan_set: null argument");
+    return TQ_ERR_INVALID;
+  }
+  const std::string k(key);
+  if (k == "graph") {            // 0: launch eagerly (e.g. inside a caller's stream capture)
+    p->plan.use_graph = value != 0;
+    return TQ_OK;
+  }
+  tq::set_error("tq_plan_set: unknown key " + k);
+  return TQ_ERR_INVALID;
+}
+
 int64_t tq_plan_query(tq_plan p, const char* key) {
   if (!p || !key) return -1;
   const tq::Plan& P = p->plan;

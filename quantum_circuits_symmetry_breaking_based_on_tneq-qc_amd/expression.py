@@ -20,7 +20,7 @@ import torch
 
 from . import _lib
 from ._lib import check, i32, i64
-from .einsum import (Network, greedy_path, linear_path, parse_equation, path_info,
+from .einsum import (Network, _State, greedy_path, linear_path, parse_equation, path_info,
                      validate_path)
 from .ops import dtype_code
 
@@ -166,6 +166,17 @@ class HipContractExpression:
             return _HipContractFn.apply(self, *tensors)
         return self._forward(*tensors, out=out, slice_range=slice_range, accumulate=accumulate)
 
+    def reverse_tree(self) -> "_ReverseTree":
+        """The per-step forward / gradient expressions used by autograd (built once)."""
+        rev = self._plans.get("reverse")
+        if rev is None:
+            with self._lock:
+                rev = self._plans.get("reverse")
+                if rev is None:
+                    rev = _ReverseTree(self)
+                    self._plans["reverse"] = rev
+        return rev
+
     def grad_expression(self, i: int) -> Tuple["HipContractExpression", List[int]]:
         """Expression for d(out)/d(operand i) contracted with grad_out:
         operands = the other inputs (conjugated by the caller) + grad_out -> operand i's modes.
@@ -225,35 +236,243 @@ class HipContractExpression:
         return out
 
 
+class _ReverseTree:
+    """Reverse-mode differentiation through the expression's pairwise path.
+
+    The reference differentiates ``oe.contract_expression(...)(*params)`` with torch autograd
+    (symmetry_breaking_quantum.py:210-224; engine_siamese.py:351-554): the forward keeps every
+    pairwise intermediate and the backward runs two contractions per pairwise step.  Same here,
+    on the HIP engine.  Step s contracts T_i, T_j -> T_k (one small native plan).  The backward
+    propagates conjugated gradients h = conj(dL/dT) (torch's complex convention
+    dT_i = dT_k . conj(T_j) becomes a plain contraction h_i = h_k . T_j), so every backward step
+    is one plain contraction: modes of T_i that neither T_k nor T_j carry (summed inside the step)
+    come back through a ones vector operand.  Cost: two pairwise steps per step instead of one
+    full-network contraction per operand.
+
+    Runtime (_TreeRuntime): intermediates and gradients live in static buffers per (dtype,
+    device); the step plans launch eagerly and, once an input-pointer set repeats (a training
+    loop updating its parameters in place), the whole forward / backward launch sequence is
+    captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed."""
+
+    def __init__(self, expr: "HipContractExpression"):
+        net = expr.net
+        sym = net.symbols
+        st = _State(net)
+        ext = net.extents
+        self.ext = ext
+        self.n_in = len(net.terms)
+        self.modes: Dict[int, Tuple[int, ...]] = {i: tuple(t) for i, t in enumerate(net.terms)}
+        self.steps = []
+        last = len(expr.path) - 1
+        s2 = lambda ms: "".join(sym[m] for m in ms)
+        shp = lambda ms: tuple(ext[m] for m in ms)
+        for s, (i, j) in enumerate(expr.path):
+            res = st.result(i, j)
+            if s == last:
+                res = tuple(net.out)      # the final step writes the output's mode order
+            k = st.contract(i, j)
+            mi, mj = self.modes[i], self.modes[j]
+            self.modes[k] = res
+            fwd = HipContractExpression(f"{s2(mi)},{s2(mj)}->{s2(res)}", shp(mi), shp(mj), optimize=[(0, 1)])
+            bwd = []
+            for a, other, m_a, m_o in ((i, j, mi, mj), (j, i, mj, mi)):
+                avail = set(res) | set(m_o)
+                extra = [m for m in m_a if m not in avail]          # broadcast back via ones
+                terms = [s2(res), s2(m_o)] + [sym[m] for m in extra]
+                shapes = [shp(res), shp(m_o)] + [(ext[m],) for m in extra]
+                nt = 2 + len(extra)          # SSA path: (0, 1), then each ones vector joins
+                path = [(0, 1)] + [(1 + t, nt + t - 1) for t in range(1, 1 + len(extra))]
+                g = HipContractExpression(",".join(terms) + "->" + s2(m_a), *shapes, optimize=path)
+                bwd.append((a, other, g, [ext[m] for m in extra]))
+            self.steps.append((i, j, k, fwd, bwd))
+        self.final = self.n_in + len(expr.path) - 1 if expr.path else 0
+        self.single = None
+        if not expr.path:   # one operand: a transpose / single-side sum of it
+            self.single = expr.grad_expression(0)
+        self._rt: Dict[tuple, "_TreeRuntime"] = {}
+
+    def runtime(self, dtype, device) -> "_TreeRuntime":
+        key = (dtype, device.index)
+        rt = self._rt.get(key)
+        if rt is None:
+            rt = self._rt[key] = _TreeRuntime(self, dtype, device)
+        return rt
+
+
+class _TreeRuntime:
+    _MAX_GRAPHS = 4
+
+    def __init__(self, tree: _ReverseTree, dtype, device):
+        self.tree, self.dtype, self.dev = tree, dtype, device
+        t = tree
+        shape = lambda n: tuple(t.ext[m] for m in t.modes[n])
+        with torch.cuda.device(device):
+            self.vals = {k: torch.empty(shape(k), dtype=dtype, device=device) for (_, _, k, _, _) in t.steps}
+            # conjugated gradients: the inputs' in one flat buffer (one conj at the end), the
+            # intermediates' separately
+            sizes = [int(torch.Size(shape(i)).numel()) for i in range(t.n_in)]
+            self.flat = torch.empty(sum(sizes), dtype=dtype, device=device)
+            self.h: Dict[int, torch.Tensor] = {}
+            off = 0
+            for i, n in enumerate(sizes):
+                self.h[i] = self.flat[off:off + n].view(shape(i))
+                off += n
+            for (_, _, k, _, _) in t.steps:
+                self.h[k] = torch.empty(shape(k), dtype=dtype, device=device)
+            self.ones = {}
+            for (_, _, _, _, bwd) in t.steps:
+                for (_, _, _, exts) in bwd:
+                    for e in exts:
+                        if e not in self.ones:
+                            self.ones[e] = torch.ones((e,), dtype=dtype, device=device)
+            # step plans: eager launches (the sequence is captured as a whole)
+            self.fplans = []
+            self.bplans = []
+            for (i, j, k, fwd, bwd) in t.steps:
+                fp = fwd.plan(dtype, None, device.index)
+                _lib.check(_lib.lib().tq_plan_set(fp._h, b"graph", 0), "tq_plan_set")
+                self.fplans.append(fp)
+                bp = []
+                for (a, other, g, exts) in bwd:
+                    pl = g.plan(dtype, None, device.index)
+                    _lib.check(_lib.lib().tq_plan_set(pl._h, b"graph", 0), "tq_plan_set")
+                    bp.append(pl)
+                self.bplans.append(bp)
+        self.gen = 0
+        self.seen: Dict[tuple, int] = {}
+        self.graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
+
+    def _val(self, n, ins):
+        return ins[n] if n < self.tree.n_in else self.vals[n]
+
+    def _fwd_eager(self, ins):
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        for (i, j, k, _, _), pl in zip(self.tree.steps, self.fplans):
+            pl.execute([self._val(i, ins).data_ptr(), self._val(j, ins).data_ptr()],
+                       self.vals[k].data_ptr(), stream)
+
+    def _bwd_eager(self, ins, need):
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        for (i, j, k, _, bwd), bps in zip(reversed(self.tree.steps), reversed(self.bplans)):
+            if not need[k]:
+                continue
+            for (a, other, _, exts), pl in zip(bwd, bps):
+                if not need[a]:
+                    continue
+                ptrs = [self.h[k].data_ptr(), self._val(other, ins).data_ptr()]
+                ptrs += [self.ones[e].data_ptr() for e in exts]
+                pl.execute(ptrs, self.h[a].data_ptr(), stream)
+
+    def _run(self, kind, key, fn):
+        """fn() eagerly; captured into a graph the second time `key` is seen, replayed after."""
+        g = self.graphs.get(key)
+        if g is not None:
+            g.replay()
+            return
+        n = self.seen.get(key, 0) + 1
+        self.seen[key] = n
+        if n < 2 or _graphs_off():
+            fn()
+            return
+        if len(self.graphs) >= self._MAX_GRAPHS:
+            self.graphs.pop(next(iter(self.graphs)))
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.dev)
+        with torch.cuda.graph(g):
+            fn()
+        self.graphs[key] = g
+        g.replay()
+
+    def forward(self, ins):
+        key = ("f",) + tuple(t.data_ptr() for t in ins)
+        self._run("f", key, lambda: self._fwd_eager(ins))
+        self.gen += 1
+        return self.vals[self.tree.final]
+
+    def backward(self, ins, grad_out, needs):
+        t = self.tree
+        need = {i: bool(needs[i]) for i in range(t.n_in)}
+        for i, j, k, _, _ in t.steps:
+            need[k] = need[i] or need[j]
+        hf = self.h[t.final]
+        g = grad_out.to(device=self.dev, dtype=self.dtype)
+        if self.dtype.is_complex:
+            torch.conj_physical(g.contiguous(), out=hf)
+        else:
+            hf.copy_(g)
+        key = ("b",) + tuple(x.data_ptr() for x in ins) + tuple(need[i] for i in range(t.n_in))
+        self._run("b", key, lambda: self._bwd_eager(ins, need))
+        res = self.flat.conj_physical() if self.dtype.is_complex else self.flat.clone()
+        out, off = [], 0
+        for i in range(t.n_in):
+            n = self.h[i].numel()
+            out.append(res[off:off + n].view(self.h[i].shape) if need[i] else None)
+            off += n
+        return out
+
+
+def _graphs_off() -> bool:
+    import os
+    return os.environ.get("TQ_GRAPH", "1") == "0"
+
+
 class _HipContractFn(torch.autograd.Function):
-    """Autograd for a HIP expression: d/d(operand i) = contraction of grad_out with the
-    conjugated other operands (torch's convention for complex einsum), each on the HIP engine."""
+    """Autograd for a HIP expression: reverse mode through the pairwise path (_ReverseTree),
+    every step and its two gradient contractions on the HIP engine."""
 
     @staticmethod
     def forward(ctx, expr, *tensors):
+        ts = [t.detach() if isinstance(t, torch.Tensor) else torch.as_tensor(t) for t in tensors]
         ctx.expr = expr
-        ctx.save_for_backward(*[t if isinstance(t, torch.Tensor) else torch.as_tensor(t) for t in tensors])
+        ctx.in_meta = [(t.dtype, t.device, tuple(t.shape)) for t in ts]
+        rev = expr.reverse_tree()
         with torch.no_grad():
-            return expr._forward(*[t.detach() if isinstance(t, torch.Tensor) else t for t in tensors])
+            if rev.single is not None:
+                ctx.save_for_backward(*ts)
+                return expr._forward(*ts)
+            dev = next((t.device for t in ts if t.device.type == "cuda"),
+                       torch.device("cuda", torch.cuda.current_device()))
+            dt = ts[0].dtype
+            for t in ts[1:]:
+                dt = torch.promote_types(dt, t.dtype)
+            dtype_code(dt)
+            ins = [t.to(device=dev, dtype=dt).resolve_conj().resolve_neg().contiguous() for t in ts]
+            for t, shp in zip(ins, expr.shapes):
+                if tuple(t.shape) != shp:
+                    raise ValueError(f"operand shape {tuple(t.shape)} does not match expression shape {shp}")
+            rt = rev.runtime(dt, dev)
+            with torch.cuda.device(dev):
+                out = rt.forward(ins).clone()
+        ctx.ins, ctx.rt, ctx.gen = ins, rt, rt.gen
+        return out
 
     @staticmethod
     def backward(ctx, grad_out):
         expr = ctx.expr
-        ts = ctx.saved_tensors
-        grads = [None]
-        for i, t in enumerate(ts):
-            if not ctx.needs_input_grad[i + 1]:
-                grads.append(None)
-                continue
-            g_expr, bcast = expr.grad_expression(i)
-            others = [torch.conj_physical(ts[j]) if ts[j].is_complex() else ts[j]
-                      for j in range(len(ts)) if j != i]
-            g = g_expr._forward(*others, grad_out.to(dtype=torch.promote_types(grad_out.dtype, t.dtype)))
+        rev = expr.reverse_tree()
+        needs = list(ctx.needs_input_grad[1:])
+        if rev.single is not None:
+            (t,) = ctx.saved_tensors
+            g_expr, bcast = rev.single
+            g = g_expr._forward(grad_out.to(dtype=torch.promote_types(grad_out.dtype, t.dtype)))
             for k in bcast:
                 g = g.unsqueeze(k)
-            g = g.expand(t.shape)
-            grads.append(g.to(device=t.device, dtype=t.dtype))
-        return tuple(grads)
+            return (None, g.expand(t.shape).to(device=t.device, dtype=t.dtype))
+        rt, ins = ctx.rt, ctx.ins
+        with torch.cuda.device(rt.dev):
+            if rt.gen != ctx.gen:        # another forward reused the static buffers: recompute
+                rt.forward(ins)
+            g = rt.backward(ins, grad_out, needs)
+        ctx.ins = None
+        out = [None]
+        for gi, (dt, dev, shape), nd in zip(g, ctx.in_meta, needs):
+            if not nd:
+                out.append(None)
+                continue
+            if not dt.is_complex and gi.is_complex():
+                gi = gi.real
+            out.append(gi.to(device=dev, dtype=dt))
+        return tuple(out)
 
 
 def contract_expression(eq: str, *shapes, optimize: PathSpec = "greedy", **kw) -> HipContractExpression:

@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""C5 bench: the symmetry-breaking training step (symmetry_breaking_quantum.py:184-230) on the
+HIP engine, complex128 (BASELINE.json configs[4]: "ansatz, fp64").
+
+Workload: the 8-qubit 5-cell brick wall (35 cores); target = the core-only contraction of the
+train.py:30-masked ansatz (15 cores); 8 pruning candidates = the full ansatz minus one core each
+(the first round of symmetry_breaking(): candidate = [idx], 34 cores), each fitted with
+SGDG(lr=1e-2, stiefel=True, momentum=0.9).  A step = for every candidate: core-only forward
+(2^16 amplitudes), fidelity loss, backward (reverse mode through the pairwise path), one SGDG
+step.  Metric: candidate training steps/s (8 per step).  On N GPUs the candidates are split
+across ranks (weak scaling, no collective: candidates are independent fits).
+
+CPU baseline ("port"): the same step with torch on the host — pairwise torch.tensordot along the
+same path (what opt_einsum's ContractExpression executes), torch autograd, and the reference's
+SGDG math (oracle/optim_ref.py) — timed on a bounded sample.
+    python scripts/c5_bench.py [--steps 20] [--warmup 3] [--cpu-steps 3]
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tneq_qc_amd.circuits import BrickWall, TRAIN_MASK  # noqa: E402
+from tneq_qc_amd.contractor import EinsumStrategy  # noqa: E402
+from tneq_qc_amd.optim import SGDG  # noqa: E402
+
+N_Q, DEPTH = 8, 10
+CANDIDATES = [0, 1, 4, 6, 7, 10, 11, 16]   # cores outside the target mask
+
+
+def setup(dev):
+    tgt_bw = BrickWall(N_Q, DEPTH, seed=5, mask=TRAIN_MASK)
+    eq_t, sh_t = EinsumStrategy.build_core_only_expression(tgt_bw.qctn)
+    ex_t = EinsumStrategy.create_contract_expression(eq_t, sh_t)
+    target = ex_t(*[torch.from_numpy(tgt_bw.cores[c]).to(dev) for c in tgt_bw.qctn.cores]).reshape(-1)
+    cands = []
+    for k, idx in enumerate(CANDIDATES):
+        bw = BrickWall(N_Q, DEPTH, seed=100 + k, mask=[idx])
+        eq, sh = EinsumStrategy.build_core_only_expression(bw.qctn)
+        expr = EinsumStrategy.create_contract_expression(eq, sh)
+        params = [torch.nn.Parameter(torch.from_numpy(bw.cores[c].copy()).to(dev)) for c in bw.qctn.cores]
+        opt = SGDG(params, lr=1e-2, stiefel=True, momentum=0.9)
+        cands.append((expr, params, opt, bw, eq))
+    return target, cands
+
+
+def fidelity_loss(out, tgt):
+    out_f = out.reshape(-1)
+    num = torch.vdot(tgt, out_f).abs() ** 2
+    den = (torch.vdot(tgt, tgt).real * torch.vdot(out_f, out_f).real).clamp_min(1e-12)
+    return 1.0 - num / den
+
+
+def gpu_step(target, cands):
+    losses = []
+    for expr, params, opt, _, _ in cands:
+        opt.zero_grad()
+        loss = fidelity_loss(expr(*params), target)
+        loss.backward()
+        opt.step()
+        losses.append(loss)
+    return losses
+
+
+def cpu_step_sample(target_np, cands, steps):
+    """torch-CPU pairwise tensordot along the same path + autograd + the reference SGDG math."""
+    from oracle.optim_ref import sgdg_step
+    from tneq_qc_amd.einsum import _State
+    tgt = torch.from_numpy(target_np)
+    items = []
+    for expr, params, _, bw, _ in cands:
+        items.append((expr, [p.detach().cpu().numpy().copy() for p in params], {}))
+    t0 = time.perf_counter()
+    n = 0
+    for _ in range(steps):
+        for expr, ps, state in items:
+            ts = [torch.tensor(p, requires_grad=True) for p in ps]
+            st = _State(expr.net)
+            vals = dict(enumerate(ts))
+            modes = {i: tuple(t) for i, t in enumerate(expr.net.terms)}
+            for s, (i, j) in enumerate(expr.path):
+                res = st.result(i, j)
+                k = st.contract(i, j)
+                mi, mj = modes[i], modes[j]
+                ci = [q for q, m in enumerate(mi) if m in mj]
+                cj = [mj.index(mi[q]) for q in ci]
+                out = torch.tensordot(vals[i], vals[j], dims=(ci, cj))
+                om = [m for m in mi if m not in mj] + [m for m in mj if m not in mi]
+                final = tuple(expr.net.out) if s == len(expr.path) - 1 else res
+                keep = [m for m in om if m in final]
+                if len(keep) != len(om):   # single-side sums
+                    out = out.sum(dim=[q for q, m in enumerate(om) if m not in final])
+                out = out.permute([keep.index(m) for m in final])
+                vals[k], modes[k] = out, final
+            loss = fidelity_loss(vals[max(vals)], tgt)
+            grads = torch.autograd.grad(loss, ts)
+            sgdg_step(ps, [g.numpy().copy() for g in grads], state, lr=1e-2, momentum=0.9, stiefel=True)
+            n += 1
+    return (time.perf_counter() - t0), n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    random.seed(0)
+    target, cands = setup(dev)
+    for _ in range(a.warmup):
+        gpu_step(target, cands)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        losses = gpu_step(target, cands)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    res = {"metric": "candidate training steps/s (forward + backward + SGDG), C5 ansatz",
+           "value": len(cands) / dt, "unit": "candidate-steps/s", "ms_per_step": dt * 1e3,
+           "candidates": len(cands), "cores_per_candidate": len(cands[0][1]), "dtype": "c128",
+           "amplitudes_per_forward": int(np.prod(cands[0][0].out_shape)),
+           "loss_after": [float(l.detach()) for l in losses]}
+    if a.cpu_steps > 0:
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        secs, n = cpu_step_sample(target.cpu().numpy(), cands, a.cpu_steps)
+        res["cpu_baseline"] = {"value": n / secs, "unit": "candidate-steps/s", "cores": torch.get_num_threads(),
+                               "kind": "port", "sample": f"{n} candidate-steps (torch CPU pairwise tensordot "
+                               "along the same path + autograd + oracle SGDG), complex128"}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
