@@ -38,8 +38,12 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-template <typename R> struct Cfg;
-template <> struct Cfg<float> {
+// Tile configuration per (real type, complex).  Measured (r02, scripts/gemm64_bench.py): wave tiles
+// of 64 x 128 (f32) / 64 x 64 (f64) for the real GEMMs drop to one wave per SIMD in this
+// register-staged, single-buffered kernel and lose 5-15 %, so every variant keeps 2 x 2 MFMA
+// tiles per wave.
+template <typename R, bool CPLX> struct Cfg;
+template <bool CPLX> struct CfgF32 {
   static constexpr int MT = 32, KT = 2;          // MFMA tile M=N and K
   static constexpr int TI = 2, TJ = 2;           // MFMA tiles per wave (rows, cols)
   static constexpr int WM = MT * TI, WN = MT * TJ;
@@ -48,7 +52,7 @@ template <> struct Cfg<float> {
   static constexpr int PAD = 0;                  // ds_read_b32 halves read distinct rows: no conflict
   static constexpr int NACC = 16;                // accumulator values per MFMA tile per lane
 };
-template <> struct Cfg<double> {
+template <bool CPLX> struct CfgF64 {
   static constexpr int MT = 16, KT = 4;
   static constexpr int TI = 2, TJ = 2;
   static constexpr int WM = MT * TI, WN = MT * TJ;
@@ -57,6 +61,10 @@ template <> struct Cfg<double> {
   static constexpr int PAD = 16;                 // rows k, k+1 of a ds_read_b64 half -> other banks
   static constexpr int NACC = 4;
 };
+template <> struct Cfg<float, false> : CfgF32<false> {};
+template <> struct Cfg<float, true> : CfgF32<true> {};
+template <> struct Cfg<double, false> : CfgF64<false> {};
+template <> struct Cfg<double, true> : CfgF64<true> {};
 
 struct GemmArgs {
   const void* A;
@@ -95,7 +103,7 @@ __device__ __forceinline__ void mfma<double>(double a, double b, f64x4& c) {
 
 template <typename R, bool CPLX, bool TA, bool TB>
 __global__ void __launch_bounds__(kThreads) gemm_kernel(GemmArgs g) {
-  using C_ = Cfg<R>;
+  using C_ = Cfg<R, CPLX>;
   using AccT = typename std::conditional<sizeof(R) == 4, f32x16, f64x4>::type;
   constexpr int EW = CPLX ? 2 : 1;                 // R values per element
   constexpr int VE = 16 / (EW * (int)sizeof(R));   // elements per 16-byte vector
@@ -592,7 +600,7 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
                  const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB,
                  double beta, void* C, int64_t ldc, int64_t sC, void* W, size_t wsb,
                  hipStream_t stream) {
-  using C_ = Cfg<R>;
+  using C_ = Cfg<R, CPLX>;
   constexpr int EW = CPLX ? 2 : 1;
   constexpr int VE = 16 / (EW * (int)sizeof(R));
   if constexpr (CPLX && sizeof(R) == 4) {
@@ -687,10 +695,14 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
 }  // namespace
 
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch) {
-  int64_t bm, bk;
-  if (dtype == TQ_F32 || dtype == TQ_C64) { bm = Cfg<float>::BM; bk = Cfg<float>::BK; }
-  else { bm = Cfg<double>::BM; bk = Cfg<double>::BK; }
-  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm) * batch;
+  int64_t bm, bn, bk;
+  switch (dtype) {
+    case TQ_F32: bm = Cfg<float, false>::BM; bn = Cfg<float, false>::BN; bk = Cfg<float, false>::BK; break;
+    case TQ_C64: bm = Cfg<float, true>::BM; bn = Cfg<float, true>::BN; bk = Cfg<float, true>::BK; break;
+    case TQ_F64: bm = Cfg<double, false>::BM; bn = Cfg<double, false>::BN; bk = Cfg<double, false>::BK; break;
+    default: bm = Cfg<double, true>::BM; bn = Cfg<double, true>::BN; bk = Cfg<double, true>::BK; break;
+  }
+  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   int s = choose_splits(tiles, K, (int)bk);
   if (dtype == TQ_C64) s = std::max(s, fast_c64_splits(1, 0, M, N, K, batch));
   if (s <= 1) return 0;

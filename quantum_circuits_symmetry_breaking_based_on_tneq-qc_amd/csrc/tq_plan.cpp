@@ -1009,6 +1009,28 @@ class Compiler {
         G.naddr[n] = (G.ndep[n] << d.logC) ^ (G.nsw[n] & cmask);
       }
     }
+    // gate fields and group tables (what the kernel used to build per workgroup)
+    for (size_t j = 0; j < c.gates.size(); ++j) {
+      const S2Gate& G = d.gate[j];
+      int32_t* gm = d.gmeta[j];
+      gm[kS2GmK] = G.K;
+      gm[kS2GmN] = G.N;
+      gm[kS2GmPass] = (int32_t)G.pass_mask;
+      for (int k = 0; k < kS2MaxK; ++k) gm[kS2GmKaddr + k] = k < G.K ? G.kaddr[k] : 0;
+      for (int n = 0; n < kS2MaxKN; ++n) gm[kS2GmNaddr + n] = n < G.N ? G.naddr[n] : 0;
+      for (int jj = 0; jj < 64; ++jj) {
+        const int half = jj >> 5, v = jj & 31;
+        uint32_t m = G.pass_mask;
+        int base = 0, sw = 0;
+        for (int t = 0; m; ++t) {
+          const int lo = __builtin_ctz(m);
+          m &= m - 1;
+          if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
+          if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
+        }
+        d.lut[j][jj] = (base << d.logC) ^ (sw & cmask);
+      }
+    }
     if (getenv("TQ_DEBUG_S2")) {
       fprintf(stderr, "S2 cols=2^%d logC=%d used=%d ld:", d.colbits, d.logC, used);
       for (int t = 0; t < d.nld; ++t) fprintf(stderr, " %lld/%x", (long long)d.ld_w[t], d.ld_code[t]);

@@ -56,7 +56,15 @@ struct S2Desc {
   int64_t w_in[kS2MaxColBits] = {}, w_out[kS2MaxColBits] = {};  // column-bit weights
   int32_t vsw[12] = {};          // swizzle vector of each position (kS2MaxPos used)
   S2Gate gate[kS2MaxGates];
+  // Built on the host (plan compile) and copied to LDS verbatim by the kernel:
+  //  lut[g][j]: LDS address part of group index bits -> (pass positions << logC) ^ swizzle, j < 32
+  //             for the low 5 pass bits, 32 + j for the high ones (XOR-linear, combined by ^)
+  //  gmeta[g][f]: K, N, pass mask, kaddr[0..3], naddr[0..7] (kS2GmK.. layout)
+  int32_t lut[kS2MaxGates][64] = {};
+  int32_t gmeta[kS2MaxGates][16] = {};
 };
+constexpr int kS2GmK = 0, kS2GmN = 1, kS2GmPass = 2, kS2GmKaddr = 3, kS2GmNaddr = kS2GmKaddr + kS2MaxK;
+static_assert(kS2GmNaddr + kS2MaxKN <= 16, "gate meta layout");
 
 struct S2Op {
   const S2Desc* desc = nullptr;

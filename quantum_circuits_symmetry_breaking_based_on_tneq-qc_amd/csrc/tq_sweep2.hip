@@ -43,7 +43,8 @@ constexpr int kLut = 64;                     // per-gate group tables: 32 entrie
 constexpr int kCf = kS2MaxK * kS2MaxKN;      // coefficient slots per gate
 // per-gate fields the gate passes read, staged in LDS: read in every pass of every chunk, they
 // must not queue behind the chunk's HBM stores (descriptor loads are vector loads)
-constexpr int kGmK = 0, kGmN = 1, kGmPass = 2, kGmKaddr = 3, kGmNaddr = kGmKaddr + kS2MaxK;
+constexpr int kGmK = kS2GmK, kGmN = kS2GmN, kGmPass = kS2GmPass, kGmKaddr = kS2GmKaddr,
+              kGmNaddr = kS2GmNaddr;
 constexpr int kGm = 16;
 constexpr int kDescWords2 = (int)(sizeof(S2Desc) / 8);
 static_assert(sizeof(S2Desc) % 8 == 0, "descriptor copy granularity");
@@ -55,6 +56,7 @@ struct S2Hot {
   int32_t ld_ha[kS2MaxSlots], st_ha[kS2MaxSlots];
 };
 static_assert(kGmNaddr + kS2MaxKN <= kGm, "gate meta layout");
+static_assert(kLut == 64, "lut layout shared with S2Desc::lut");
 
 #ifdef TQ_S2_TIMING
 // development instrumentation (built only with -DTQ_S2_TIMING): workgroup 0 of every op records
@@ -254,32 +256,9 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     hot.w_in[i] = ds->w_in[i];
     hot.w_out[i] = ds->w_out[i];
   }
-  // ---- gate fields -> LDS
-  for (int i = tid; i < ngates * kGm; i += NT) {
-    const S2Gate& gt = ds->gate[i / kGm];
-    const int f = i % kGm;
-    int v = 0;
-    if (f == kGmK) v = gt.K;
-    else if (f == kGmN) v = gt.N;
-    else if (f == kGmPass) v = (int)gt.pass_mask;
-    else if (f < kGmNaddr) v = gt.kaddr[f - kGmKaddr];
-    else if (f < kGmNaddr + kS2MaxKN) v = gt.naddr[f - kGmNaddr];
-    gmeta[i] = v;
-  }
-  // ---- group tables -> LDS: LDS address part (positions << logC) ^ swizzle of the pass bits of a
-  // group index, split into its low 5 and high bits (both parts are XOR-linear, so they combine by ^)
-  for (int i = tid; i < ngates * kLut; i += NT) {
-    const int g = i / kLut, j = i % kLut, half = j >> 5, v = j & 31;
-    uint32_t m = ds->gate[g].pass_mask;
-    int base = 0, sw = 0;
-    for (int t = 0; m; ++t) {
-      const int lo = __builtin_ctz(m);
-      m &= m - 1;
-      if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= ds->vsw[lo]; }
-      if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= ds->vsw[lo]; }
-    }
-    lut[i] = (base << logC) ^ (sw & cm);
-  }
+  // ---- gate fields and group tables -> LDS (built on the host, S2Desc::gmeta / lut)
+  for (int i = tid; i < ngates * kGm; i += NT) gmeta[i] = ds->gmeta[i / kGm][i % kGm];
+  for (int i = tid; i < ngates * kLut; i += NT) lut[i] = ds->lut[i / kLut][i % kLut];
   // ---- per-thread part of the load / store enumerations (low LOG_NT chunk bits); threads
   // beyond a small chunk duplicate element tid % n (same value to the same place)
   int64_t ldm = 0, stm = 0;
