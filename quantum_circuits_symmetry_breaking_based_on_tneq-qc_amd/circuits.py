@@ -164,8 +164,10 @@ class AmplitudeTask:
 
 def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Optional[Dict[int, int]] = None,
                    cut: Optional[int] = None, n_slice: int = 0, bit_seed: int = 7,
-                   absorb_vectors: bool = True) -> AmplitudeTask:
-    """Build the amplitude network; fixed bits default to a seeded uniform bitstring."""
+                   absorb_vectors: bool = True, tile: int = 4) -> AmplitudeTask:
+    """Build the amplitude network; fixed bits default to a seeded uniform bitstring.
+    With a cut, each half is swept in diamond tiles of `tile` x `tile` gates (diamond_order;
+    0 = line by line)."""
     n = circ.n_qubits
     open_set = set(int(q) for q in open_qubits)
     if fixed_bits is None:
@@ -222,8 +224,12 @@ def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Opti
                 side[i] = side[owner[net.terms[i][0]]]
         left = [i for i in range(len(kinds)) if side[i]]
         right = [i for i in range(len(kinds)) if not side[i]]
-        lord = sorted(left, key=lambda i: sweep_key(kinds[i], True))
-        rord = sorted(right, key=lambda i: sweep_key(kinds[i], False))
+        if tile:
+            lord = diamond_order(circ, kinds, net, left, True, cut - 1, tile)
+            rord = diamond_order(circ, kinds, net, right, False, cut, tile)
+        else:
+            lord = sorted(left, key=lambda i: sweep_key(kinds[i], True))
+            rord = sorted(right, key=lambda i: sweep_key(kinds[i], False))
         path = partition_path(net, [left, right], [lord, rord], pre=pre)
         lm = set(m for i in left for m in net.terms[i])
         rm = set(m for i in right for m in net.terms[i])
@@ -231,6 +237,45 @@ def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Opti
         sliced_ids = choose_slices(net, path, n_slice, cut_modes) if n_slice else []
     return AmplitudeTask(circ, eq, shapes, operands, kinds, list(open_q), dict(fixed_bits), path,
                          [net.symbols[m] for m in sliced_ids], cut)
+
+
+def diamond_order(circ: BrickWall, kinds, net: Network, ids: Sequence[int], upward: bool,
+                  boundary_pair: int, tile: int) -> List[int]:
+    """Sweep order of one half of a cut brick wall in diamond tiles.
+
+    Gate (pair r, time t) takes its two line-r legs from gates (r-1, t-1) and (r-1, t+1)
+    (r counted away from the half's far edge).  In the rotated coordinates a = (t+r-p)/2,
+    d = (r-t-p)/2 those are (a-1, d) and (a, d-1), so tiles of tile x tile gates taken in order
+    of (A+D, A) and row-major inside are a valid sweep, and a tile only ever holds 2*tile live
+    legs of the running tensor: one butterfly-sweep op (tq_sweep2) absorbs tile^2 gates where
+    the line-by-line order fits tile.  The gates on the cut's pair (whose legs the slicing
+    fixes) come last, in time order, so everything before them is slice-invariant."""
+    n = circ.n_qubits
+    owner = {}
+    for i in ids:
+        if kinds[i][0] == "core":
+            for m in net.terms[i]:
+                owner[m] = i
+    par = {(circ.core_time[kinds[i][1]] + circ.core_qubits[kinds[i][1]][0]) % 2
+           for i in ids if kinds[i][0] == "core"}
+    p = par.pop() if len(par) == 1 else 0
+
+    def core_key(i):
+        lo = circ.core_qubits[kinds[i][1]][0]
+        t = circ.core_time[kinds[i][1]]
+        if lo == boundary_pair:
+            return (1, t, 0, 0, 0)
+        r = lo if upward else (n - 2) - lo
+        a, d = (t + r - p) // 2, (r - t - p) // 2
+        A, D = a // tile, d // tile
+        return (0, A + D, A, a, d)
+
+    def key(i):
+        if kinds[i][0] == "core":
+            return core_key(i) + (0,)
+        return core_key(owner[net.terms[i][0]]) + (-1 if kinds[i][0] == "in" else 1,)
+
+    return sorted(ids, key=key)
 
 
 # ---- the BASELINE.json configurations ------------------------------------------------------

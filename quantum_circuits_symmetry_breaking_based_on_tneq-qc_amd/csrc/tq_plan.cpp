@@ -768,6 +768,13 @@ class Compiler {
     }();
     return v;
   }
+  static bool s2_blocks_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_BLOCKS");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
   static bool s2_enabled() {
     static const int v = [] {
       const char* e = getenv("TQ_SWEEP2");
@@ -1031,6 +1038,86 @@ class Compiler {
         d.lut[j][jj] = (base << d.logC) ^ (sw & cmask);
       }
     }
+    // passes: register blocks of consecutive square gates (S2Desc::pmeta), single gates otherwise
+    {
+      const int ng = (int)c.gates.size();
+      const int B = s2_block_bits((int)P_.esz, int64_t(1) << (d.logC + used));
+      auto kmask_of = [&](int j) {
+        uint32_t m = 0;
+        for (int k = 0; k < d.gate[j].K; ++k) m |= (uint32_t)kdep[j][k];
+        return m;
+      };
+      auto square = [&](int j) {
+        const S2Gate& G = d.gate[j];
+        if (G.K != G.N || (G.K != 2 && G.K != 4)) return false;
+        for (int k = 0; k < G.K; ++k) if (kdep[j][k] != ndep[j][k]) return false;
+        return true;
+      };
+      auto group_lut = [&](uint32_t pass_mask, int32_t* lut) {
+        for (int jj = 0; jj < 64; ++jj) {
+          const int half = jj >> 5, v = jj & 31;
+          uint32_t m = pass_mask;
+          int base = 0, sw = 0;
+          for (int t = 0; m; ++t) {
+            const int lo = __builtin_ctz(m);
+            m &= m - 1;
+            if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
+            if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
+          }
+          lut[jj] = (base << d.logC) ^ (sw & cmask);
+        }
+      };
+      const bool blocks = s2_blocks_enabled();
+      int j = 0;
+      d.npass = 0;
+      while (j < ng) {
+        int32_t* pm = d.pmeta[d.npass++];
+        pm[kS2PmFirst] = j;
+        int e = j + 1;
+        uint32_t bm = 0, live = 0;
+        if (blocks && square(j)) {
+          bm = kmask_of(j);
+          live = d.gate[j].pass_mask | bm;
+          while (e < ng && e - j < kS2BlkMaxGates && square(e) &&
+                 __builtin_popcount(bm | kmask_of(e)) <= B)
+            bm |= kmask_of(e), ++e;
+        }
+        if (e - j >= 2) {
+          // pad the block with untouched live positions up to B bits (fewer, larger groups)
+          for (int q = 0; q < kS2MaxPos && __builtin_popcount(bm) < B; ++q)
+            if (((live >> q) & 1) && !((bm >> q) & 1)) bm |= 1u << q;
+          if (__builtin_popcount(bm) != B) e = j + 1;
+        }
+        if (e - j < 2) {
+          pm[kS2PmCount] = 1;
+          pm[kS2PmB] = 0;
+          j += 1;
+          continue;
+        }
+        pm[kS2PmCount] = e - j;
+        pm[kS2PmB] = B;
+        pm[kS2PmPass] = (int32_t)(live & ~bm);
+        int bp[4], nb = 0;
+        for (int q = 0; q < kS2MaxPos; ++q)
+          if ((bm >> q) & 1) bp[nb++] = q;
+        for (int b = 0; b < B; ++b)
+          pm[kS2PmAddr + b] = ((1 << bp[b]) << d.logC) ^ (d.vsw[bp[b]] & cmask);
+        auto local = [&](int pos) {
+          for (int b = 0; b < B; ++b) if (bp[b] == pos) return b;
+          return -1;
+        };
+        for (int q = j; q < e; ++q) {
+          const S2Gate& G = d.gate[q];
+          // index bit t of the gate <-> position of input k = 1 << t
+          const int i0 = local(__builtin_ctz((uint32_t)kdep[q][1]));
+          int code = i0;
+          if (G.K == 4) code |= (local(__builtin_ctz((uint32_t)kdep[q][2])) << 2) | 16;
+          pm[kS2PmCode + (q - j)] = code;
+        }
+        group_lut(live & ~bm, d.lut[j]);
+        j = e;
+      }
+    }
     if (getenv("TQ_DEBUG_S2")) {
       fprintf(stderr, "S2 cols=2^%d logC=%d used=%d ld:", d.colbits, d.logC, used);
       for (int t = 0; t < d.nld; ++t) fprintf(stderr, " %lld/%x", (long long)d.ld_w[t], d.ld_code[t]);
@@ -1118,7 +1205,9 @@ class Compiler {
       std::ostringstream o;
       o << "step " << c.gates.front().step << ".." << op.step << " SWEEP2 gates=" << c.gates.size()
         << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " C=" << (1 << d.logC)
-        << " chunks=" << d.nchunks << (direct ? " ->OUT" : "");
+        << " chunks=" << d.nchunks << (direct ? " ->OUT" : "") << " KxN=";
+      for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
+      o << " passes=" << d.npass;
       op.note = o.str();
       P_.ops.push_back(op);
       res.modes = c.out_modes;

@@ -62,9 +62,25 @@ struct S2Desc {
   //  gmeta[g][f]: K, N, pass mask, kaddr[0..3], naddr[0..7] (kS2GmK.. layout)
   int32_t lut[kS2MaxGates][64] = {};
   int32_t gmeta[kS2MaxGates][16] = {};
+  // Passes over the tile (one barrier each).  A pass is one gate, or a register block: a run of
+  // consecutive square gates (K == N, outputs on their inputs' positions) whose positions fit B
+  // bits; every thread then holds 2^B elements of a group in registers and applies the whole
+  // run to them (one LDS read + write per element for the run instead of per gate).
+  //  pmeta[p]: first gate, gate count, B (0 = single gate), pass mask (live positions outside the
+  //            block), block-bit address parts [4, 4+B), per-gate local codes [8, 8+count):
+  //            bits 0-1 / 2-3 = block bits of the gate's index bits 0 / 1, bit 4 = 4x4 (else 2x2)
+  //  a block's group table replaces lut[first gate]
+  int32_t npass = 0, pad2 = 0;
+  int32_t pmeta[kS2MaxGates][16] = {};
 };
 constexpr int kS2GmK = 0, kS2GmN = 1, kS2GmPass = 2, kS2GmKaddr = 3, kS2GmNaddr = kS2GmKaddr + kS2MaxK;
 static_assert(kS2GmNaddr + kS2MaxKN <= 16, "gate meta layout");
+constexpr int kS2PmFirst = 0, kS2PmCount = 1, kS2PmB = 2, kS2PmPass = 3, kS2PmAddr = 4, kS2PmCode = 8;
+constexpr int kS2BlkMaxGates = 8;      // gates per register block
+inline int s2_block_bits(int esz, int64_t tile_elems) {
+  // 2^B elements per thread: 16 (FP32 data, tiles of >= 8192 elements) or 8
+  return (esz <= 8 && tile_elems >= 8192) ? 4 : 3;
+}
 
 struct S2Op {
   const S2Desc* desc = nullptr;

@@ -116,15 +116,19 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
                                           const int32_t* __restrict__ gm,
                                           const int32_t* __restrict__ lut, int logC) {
   constexpr int U = sizeof(T) > 8 ? (K * N >= 8 ? 1 : 2) : (K * N >= 16 ? 2 : 4);
-  constexpr bool kReg = K * N * sizeof(T) <= 64;   // coefficients held in registers
+  // coefficients held in registers (up to 32 VGPRs for FP32 data, 16 for FP64); larger gates
+  // re-read them from LDS per group
+  constexpr bool kReg = K * N * sizeof(T) <= (sizeof(typename Traits<T>::R) == 4 ? 128 : 64);
+  constexpr int SH = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;   // element -> byte offset
+  char* const bb = reinterpret_cast<char*>(buf);
   const int tid = threadIdx.x;
   const int ngroups = (1 << logC) << __popc((uint32_t)gm[kGmPass]);
-  const int cm = (1 << logC) - 1;
-  int ka[K], na[N];
+  const int cmb = ((1 << logC) - 1) << SH;
+  int ka[K], na[N];   // byte offsets (the LUT entries are staged as byte offsets too)
 #pragma unroll
-  for (int k = 0; k < K; ++k) ka[k] = gm[kGmKaddr + k];
+  for (int k = 0; k < K; ++k) ka[k] = gm[kGmKaddr + k] << SH;
 #pragma unroll
-  for (int n = 0; n < N; ++n) na[n] = gm[kGmNaddr + n];
+  for (int n = 0; n < N; ++n) na[n] = gm[kGmNaddr + n] << SH;
   T creg[kReg ? K * N : 1];
   if constexpr (kReg) {
 #pragma unroll
@@ -142,13 +146,13 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
       ok[u] = gi < ngroups;
       gi = ok[u] ? gi : g0;
       const int gp = gi >> logC;
-      a0[u] = lut[gp & 31] ^ lut[32 + (gp >> 5)] ^ (gi & cm);
+      a0[u] = lut[gp & 31] ^ lut[32 + (gp >> 5)] ^ ((gi << SH) & cmb);
     }
     T x[U][K];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < K; ++k) x[u][k] = buf[a0[u] ^ ka[k]];
+      for (int k = 0; k < K; ++k) x[u][k] = *reinterpret_cast<const T*>(bb + (a0[u] ^ ka[k]));
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       T c[K];
@@ -165,9 +169,132 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
         T acc = tzero<T>();
 #pragma unroll
         for (int k = 0; k < K; ++k) mac(acc, x[u][k], c[k]);
-        if (ok[u]) buf[a0[u] ^ na[n]] = acc;
+        if (ok[u]) *reinterpret_cast<T*>(bb + (a0[u] ^ na[n])) = acc;
       }
     }
+  }
+}
+
+// ---- register blocks (S2Desc::pmeta): a run of square gates applied to 2^B elements per group
+// held in registers.  Block bit b of element e is bit b of e; a gate's index bits 0 / 1 sit on
+// block bits I / J (compile-time, one instantiation per placement).
+template <int B, int I, int J>
+__device__ __forceinline__ constexpr int deposit2(int r) {
+  // bits of r into the block bits other than I and J, ascending
+  int v = 0, t = 0;
+  for (int b = 0; b < B; ++b) {
+    if (b == I || b == J) continue;
+    v |= ((r >> t) & 1) << b;
+    ++t;
+  }
+  return v;
+}
+
+// wave-uniform value -> scalar registers (the block passes keep their VGPRs for the elements)
+template <typename T>
+__device__ __forceinline__ T uniform(T v) {
+  static_assert(sizeof(T) % 4 == 0, "dword granularity");
+  union { T t; int w[sizeof(T) / 4]; } u;
+  u.t = v;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) u.w[i] = __builtin_amdgcn_readfirstlane(u.w[i]);
+  return u.t;
+}
+
+template <typename T, int B, int I, int J>
+__device__ __forceinline__ void blk_apply4(T (&x)[1 << B], const T* __restrict__ cf) {
+  T c[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c[i] = uniform(cf[i]);
+#pragma unroll
+  for (int r = 0; r < (1 << (B - 2)); ++r) {
+    const int base = deposit2<B, I, J>(r);
+    T in[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) in[k] = x[base | ((k & 1) << I) | ((k >> 1) << J)];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      T acc = tzero<T>();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mac(acc, in[k], c[k * 4 + n]);
+      x[base | ((n & 1) << I) | ((n >> 1) << J)] = acc;
+    }
+  }
+}
+
+template <typename T, int B, int I>
+__device__ __forceinline__ void blk_apply2(T (&x)[1 << B], const T* __restrict__ cf) {
+  T c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = uniform(cf[i]);
+#pragma unroll
+  for (int r = 0; r < (1 << (B - 1)); ++r) {
+    const int base = deposit2<B, I, I>(r) ;
+    const T a = x[base], b = x[base | (1 << I)];
+    T y0 = tzero<T>(), y1 = tzero<T>();
+    mac(y0, a, c[0]);
+    mac(y0, b, c[2]);
+    mac(y1, a, c[1]);
+    mac(y1, b, c[3]);
+    x[base] = y0;
+    x[base | (1 << I)] = y1;
+  }
+}
+
+template <typename T, int B>
+__device__ __forceinline__ void blk_gate(T (&x)[1 << B], const T* cf, int code) {
+#define TQ_B4(i, j) case 16 | (j << 2) | i: blk_apply4<T, B, i, j>(x, cf); break;
+#define TQ_B2(i) case i: blk_apply2<T, B, i>(x, cf); break;
+  if constexpr (B == 4) {
+    switch (code) {
+      TQ_B4(0, 1) TQ_B4(0, 2) TQ_B4(0, 3) TQ_B4(1, 0) TQ_B4(1, 2) TQ_B4(1, 3)
+      TQ_B4(2, 0) TQ_B4(2, 1) TQ_B4(2, 3) TQ_B4(3, 0) TQ_B4(3, 1) TQ_B4(3, 2)
+      TQ_B2(0) TQ_B2(1) TQ_B2(2) TQ_B2(3)
+      default: break;
+    }
+  } else {
+    switch (code) {
+      TQ_B4(0, 1) TQ_B4(0, 2) TQ_B4(1, 0) TQ_B4(1, 2) TQ_B4(2, 0) TQ_B4(2, 1)
+      TQ_B2(0) TQ_B2(1) TQ_B2(2)
+      default: break;
+    }
+  }
+#undef TQ_B4
+#undef TQ_B2
+}
+
+template <typename T, int B>
+__device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restrict__ cf_all,
+                                           const int32_t* __restrict__ pm,
+                                           const int32_t* __restrict__ lut, int logC) {
+  constexpr int E = 1 << B;
+  constexpr int SH = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;
+  char* const bb = reinterpret_cast<char*>(buf);
+  const int ngroups = (1 << logC) << __popc((uint32_t)pm[kS2PmPass]);
+  const int cmb = ((1 << logC) - 1) << SH;
+  // block-bit address parts are wave-uniform: scalar registers, element offsets formed by SALU
+  int ba[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) ba[b] = __builtin_amdgcn_readfirstlane(pm[kS2PmAddr + b] << SH);
+  auto off = [&](int e) {
+    int o = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+      if ((e >> b) & 1) o ^= ba[b];
+    return o;
+  };
+  const int first = pm[kS2PmFirst], cnt = pm[kS2PmCount];
+  for (int g0 = threadIdx.x; g0 < ngroups; g0 += NT) {
+    const int gp = g0 >> logC;
+    int a0 = lut[gp & 31] ^ lut[32 + (gp >> 5)] ^ ((g0 << SH) & cmb);
+    T x[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = *reinterpret_cast<const T*>(bb + (a0 ^ off(e)));
+    // the element addresses are recomputed for the write-back (not held across the gates)
+    asm volatile("" : "+v"(a0));
+    for (int q = 0; q < cnt; ++q) blk_gate<T, B>(x, cf_all + (first + q) * kCf, pm[kS2PmCode + q]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) *reinterpret_cast<T*>(bb + (a0 ^ off(e))) = x[e];
   }
 }
 
@@ -188,11 +315,17 @@ __device__ __forceinline__ void run_gate(T* buf, const T* cf, const int32_t* gm,
 template <typename T, int CB>
 __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   constexpr int RMAX = (1 << CB) / NT;
+  // register copies of elements as plain vector words (16-byte struct arrays behind runtime
+  // conditions are otherwise demoted to scratch)
+  using Raw = typename std::conditional<sizeof(T) == 16, double __attribute__((ext_vector_type(2))),
+                                        typename std::conditional<sizeof(T) == 8, double, float>::type>::type;
+  static_assert(sizeof(Raw) == sizeof(T), "raw slot word");
   static_assert(RMAX <= kS2MaxSlots, "register slots");
   __shared__ T buf[1 << CB];
   __shared__ int32_t lut[kS2MaxGates * kLut];            // group -> LDS address part
   __shared__ T cf[kS2MaxGates * kCf];                    // gate coefficients, k*N+n
   __shared__ int32_t gmeta[kS2MaxGates * kGm];           // K, N, pass mask, kaddr, naddr
+  __shared__ int32_t pmeta[kS2MaxGates * 16];            // passes (S2Desc::pmeta)
   __shared__ S2Hot hot;
   const int tid = threadIdx.x;
   // ---- which op this workgroup works on (wave-uniform scan over <= 16 ranges)
@@ -219,16 +352,38 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   {
     const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(d);
     uint2* bd = reinterpret_cast<uint2*>(buf);
-    for (int i = tid; i < kDescWords2; i += NT) bd[i] = gd[i];
-    for (int i = tid; i < kS2MaxGates * kS2GateRaw; i += NT) {
+    // every load is issued before the first LDS store (one memory round trip, not one per
+    // loop iteration)
+    constexpr int kIt = (kDescWords2 + NT - 1) / NT, kGt = (kS2MaxGates * kS2GateRaw + NT - 1) / NT;
+    uint2 dw[kIt];
+    Raw gw[kGt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + it * NT;
+      if (i < kDescWords2) dw[it] = gd[i];
+    }
+#pragma unroll
+    for (int it = 0; it < kGt; ++it) {
+      const int i = tid + it * NT;
       const int g = i / kS2GateRaw, e = i % kS2GateRaw;
-      if (e < (int)op.gnum[g]) graw[i] = reinterpret_cast<const T*>(op.G[g])[e];
+      if (i < kS2MaxGates * kS2GateRaw && e < (int)op.gnum[g]) gw[it] = reinterpret_cast<const Raw*>(op.G[g])[e];
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + it * NT;
+      if (i < kDescWords2) bd[i] = dw[it];
+    }
+#pragma unroll
+    for (int it = 0; it < kGt; ++it) {
+      const int i = tid + it * NT;
+      const int g = i / kS2GateRaw, e = i % kS2GateRaw;
+      if (i < kS2MaxGates * kS2GateRaw && e < (int)op.gnum[g]) reinterpret_cast<Raw*>(graw)[i] = gw[it];
     }
   }
   const T* __restrict__ X = reinterpret_cast<const T*>(op.X);
   T* __restrict__ Y = reinterpret_cast<T*>(op.Y);
   const int lb = (int)blockIdx.x - op.block_begin, nb = op.nblocks;
-  const int logC = d->logC, colbits = d->colbits, ngates = d->ngates;
+  const int logC = d->logC, colbits = d->colbits, npass = d->npass;
   const int cm = (1 << logC) - 1;
   const int64_t nchunks = d->nchunks;
   const int nld = d->nld, nst = d->nst;
@@ -239,6 +394,106 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   __syncthreads();
   TQ_TS(1);
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
+  const int ngates = ds->ngates;
+  // ---- per-thread part of the load / store enumerations (low LOG_NT chunk bits); threads
+  // beyond a small chunk duplicate element tid % n (same value to the same place)
+  int64_t ldm = 0, stm = 0;
+  int lda = 0, sta = 0;
+  {
+    const int ti = tid & (nin - 1), to = tid & (nout - 1);
+#pragma unroll
+    for (int b = 0; b < LOG_NT; ++b) {
+      const int64_t lw = ds->ld_w[b], sw = ds->st_w[b];
+      const int la = ds->ld_a[b], sa = ds->st_a[b];
+      const bool lb_on = b < nld && ((ti >> b) & 1), sb_on = b < nst && ((to >> b) & 1);
+      ldm += lb_on ? lw : 0;
+      lda ^= lb_on ? la : 0;
+      stm += sb_on ? sw : 0;
+      sta ^= sb_on ? sa : 0;
+    }
+  }
+  const bool st_lane = tid < nout;
+  // uniform part (chunk + register slot) in scalar registers, lane part as a 32-bit byte offset
+  const uint32_t ldo = (uint32_t)(ldm * (int64_t)sizeof(T)), sto = (uint32_t)(stm * (int64_t)sizeof(T));
+  auto chunk_base = [&](int64_t ch, const int64_t* w) {
+    int64_t o = 0;
+    for (int b = logC; b < colbits; ++b)
+      if ((ch >> (b - logC)) & 1) o += w[b];
+    return o;
+  };
+  // Chunk base offsets of this workgroup's chunks lb + i*nb, i < 64: lane i of every wave holds
+  // chunk i's (built once, all column-bit weights read in one batch); the chunk loop takes them
+  // with a lane read instead of a chain of dependent LDS reads per chunk.
+  const int64_t nloc = (nchunks - lb + nb - 1) / nb;
+  const bool lane_bases = nloc <= 64;
+  int64_t cb_in = 0, cb_out = 0;
+  {
+    const int64_t chl = lb + (int64_t)(tid & 63) * nb;
+    for (int b0 = logC & ~7; b0 < colbits; b0 += 8) {   // batches of 8 weights in flight
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int b = b0 + q;
+        const int bb = b < kS2MaxColBits ? b : kS2MaxColBits - 1;
+        const int64_t wi = ds->w_in[bb], wo = ds->w_out[bb];
+        const bool on = b >= logC && b < colbits && ((chl >> (b - logC)) & 1);
+        cb_in += on ? wi : 0;
+        cb_out += on ? wo : 0;
+      }
+    }
+  }
+  auto lane64 = [](int64_t v, int i) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, i);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), i);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  };
+  auto base_in = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_in, i) : chunk_base(ch, hot.w_in); };
+  auto base_out = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_out, i) : chunk_base(ch, hot.w_out); };
+  // The first chunk is loaded into RMAX register slots before the tables are staged (those
+  // registers are free again before the gate passes).  Inside the chunk loop only chunks of at
+  // most RPF slots are prefetched under the gate passes (the register-block passes need the
+  // VGPRs); such ops are the multi-chunk ones (small input tile, large output tile).  Larger
+  // chunks are loaded when they enter the tile.
+  constexpr int RPF = RMAX > 2 ? 2 : RMAX;
+  Raw reg[RPF];
+  const bool pf = rin <= RPF;
+  Raw* const bufr = reinterpret_cast<Raw*>(buf);
+  const Raw* const Xr = reinterpret_cast<const Raw*>(X);
+  // slot loops run a compile-time count (a power of two): loads / LDS accesses issue back to back
+#define TQ_SLOTS(CAP, R, BODY)                                   \
+  if constexpr ((CAP) >= (R)) {                                  \
+    _Pragma("unroll") for (int r = 0; r < (R); ++r) BODY;        \
+  }
+#define TQ_BY_COUNT(CAP, n, BODY)                                \
+  do {                                                           \
+    if ((n) >= 16) { TQ_SLOTS(CAP, 16, BODY) }                   \
+    else if ((n) >= 8) { TQ_SLOTS(CAP, 8, BODY) }                \
+    else if ((n) >= 4) { TQ_SLOTS(CAP, 4, BODY) }                \
+    else if ((n) >= 2) { TQ_SLOTS(CAP, 2, BODY) }                \
+    else { TQ_SLOTS(CAP, 1, BODY) }                              \
+  } while (0)
+  auto prefetch = [&](int i, int64_t ch) {
+    if (!pf) return;
+    const int64_t base = base_in(i, ch);
+    TQ_BY_COUNT(RPF, rin, reg[r] = *lane_at(Xr + uniform(base + hot.ld_hm[r]), ldo));
+  };
+  auto fill = [&](int i, int64_t ch) {   // the chunk's elements -> tile
+    if (pf) {
+      TQ_BY_COUNT(RPF, rin, bufr[lda ^ hot.ld_ha[r]] = reg[r]);
+      return;
+    }
+    const int64_t base = base_in(i, ch);
+    Raw t[RMAX];
+    TQ_BY_COUNT(RMAX, rin, t[r] = *lane_at(Xr + uniform(base + hot.ld_hm[r]), ldo));
+    TQ_BY_COUNT(RMAX, rin, bufr[lda ^ hot.ld_ha[r]] = t[r]);
+  };
+  Raw reg0[RMAX];
+  // ---- the first chunk's loads go out now (addresses from the staged descriptor) and land
+  // while the tables are staged
+  int64_t ch = lb;
+  if (ch < nchunks) {
+    const int64_t base = lane_bases ? lane64(cb_in, 0) : chunk_base(ch, ds->w_in);
+    TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + ds->ld_hm[r]), ldo));
+  }
   // ---- gate coefficients -> LDS
   for (int i = tid; i < ngates * kCf; i += NT) {
     const int g = i / kCf, t = i % kCf;
@@ -256,72 +511,40 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     hot.w_in[i] = ds->w_in[i];
     hot.w_out[i] = ds->w_out[i];
   }
-  // ---- gate fields and group tables -> LDS (built on the host, S2Desc::gmeta / lut)
+  // ---- gate fields and group tables -> LDS (built on the host, S2Desc::gmeta / lut; the
+  // LUT entries become byte offsets)
   for (int i = tid; i < ngates * kGm; i += NT) gmeta[i] = ds->gmeta[i / kGm][i % kGm];
-  for (int i = tid; i < ngates * kLut; i += NT) lut[i] = ds->lut[i / kLut][i % kLut];
-  // ---- per-thread part of the load / store enumerations (low LOG_NT chunk bits); threads
-  // beyond a small chunk duplicate element tid % n (same value to the same place)
-  int64_t ldm = 0, stm = 0;
-  int lda = 0, sta = 0;
-  {
-    const int ti = tid & (nin - 1), to = tid & (nout - 1);
-    for (int b = 0; b < LOG_NT; ++b) {
-      if (b < nld && ((ti >> b) & 1)) { ldm += ds->ld_w[b]; lda ^= ds->ld_a[b]; }
-      if (b < nst && ((to >> b) & 1)) { stm += ds->st_w[b]; sta ^= ds->st_a[b]; }
-    }
-  }
-  const bool st_lane = tid < nout;
-  // uniform part (chunk + register slot) in scalar registers, lane part as a 32-bit byte offset
-  const uint32_t ldo = (uint32_t)(ldm * (int64_t)sizeof(T)), sto = (uint32_t)(stm * (int64_t)sizeof(T));
-  __syncthreads();
+  for (int i = tid; i < npass * 16; i += NT) pmeta[i] = ds->pmeta[i / 16][i % 16];
+  constexpr int kSh = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;
+  for (int i = tid; i < ngates * kLut; i += NT) lut[i] = ds->lut[i / kLut][i % kLut] << kSh;
+  __syncthreads();   // every wave is done with the descriptor copy: the tile may be written
   TQ_TS(2);
-  auto chunk_base = [&](int64_t ch, const int64_t* w) {
-    int64_t o = 0;
-    for (int b = logC; b < colbits; ++b)
-      if ((ch >> (b - logC)) & 1) o += w[b];
-    return o;
-  };
-  T reg[RMAX];
-  // slot loops run a compile-time count (a power of two): loads / LDS accesses issue back to back
-#define TQ_SLOTS(R, BODY)                                  \
-  if constexpr (RMAX >= (R)) {                             \
-    _Pragma("unroll") for (int r = 0; r < (R); ++r) BODY;  \
-  }
-#define TQ_BY_COUNT(n, BODY)                                     \
-  do {                                                           \
-    if ((n) >= 16) { TQ_SLOTS(16, BODY) }                        \
-    else if ((n) >= 8) { TQ_SLOTS(8, BODY) }                     \
-    else if ((n) >= 4) { TQ_SLOTS(4, BODY) }                     \
-    else if ((n) >= 2) { TQ_SLOTS(2, BODY) }                     \
-    else { TQ_SLOTS(1, BODY) }                                   \
-  } while (0)
-  auto prefetch = [&](int64_t ch) {
-    const int64_t base = chunk_base(ch, hot.w_in);
-    TQ_BY_COUNT(rin, reg[r] = *lane_at(X + base + hot.ld_hm[r], ldo));
-  };
   // Chunk pipeline.  On this ISA one counter (vmcnt) covers loads and stores, and a wait for a
   // load issued before some stores waits for those stores too (they may complete out of order),
   // so the order below keeps every wait where nothing else is pending:
   //   next chunk's loads -> gate passes -> wait(all) -> store this chunk -> tile <- next chunk
   // the stores of a chunk then drain under the next chunk's gate passes and the loads of the
   // chunk after it, instead of being waited for before that chunk can enter the tile.
-  int64_t ch = lb;
-  if (ch < nchunks) {
-    prefetch(ch);
-    TQ_BY_COUNT(rin, buf[lda ^ hot.ld_ha[r]] = reg[r]);
-  }
+  if (ch < nchunks) TQ_BY_COUNT(RMAX, rin, bufr[lda ^ hot.ld_ha[r]] = reg0[r]);
   __syncthreads();
   TQ_TS(3);
 #ifdef TQ_S2_TIMING
   const unsigned long long clk0 = clock64();
   unsigned long long clk_gates = 0;
 #endif
-  for (; ch < nchunks; ch += nb) {
+  for (int i = 0; ch < nchunks; ch += nb, ++i) {
     const int64_t nxt = ch + nb;
     const bool more = nxt < nchunks;
-    if (more) prefetch(nxt);
-    for (int g = 0; g < ngates; ++g) {
-      run_gate<T>(buf, cf + g * kCf, gmeta + g * kGm, lut + g * kLut, logC);
+    if (more) prefetch(i + 1, nxt);
+    for (int p = 0; p < npass; ++p) {
+      const int32_t* pm = pmeta + p * 16;
+      const int g = pm[kS2PmFirst];
+      const int bk = pm[kS2PmB];
+      if (bk == 0) run_gate<T>(buf, cf + g * kCf, gmeta + g * kGm, lut + g * kLut, logC);
+      else if (bk == 4) {
+        if constexpr (sizeof(T) <= 8) block_pass<T, 4>(buf, cf, pm, lut + g * kLut, logC);
+      }
+      else block_pass<T, 3>(buf, cf, pm, lut + g * kLut, logC);
       __syncthreads();
     }
     if (ch == lb) TQ_TS(4);
@@ -331,7 +554,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     // vmcnt(0) (expcnt / lgkmcnt unconstrained): the next chunk is in registers, the previous
     // chunk's stores are done
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    const int64_t base = chunk_base(ch, hot.w_out);
+    const int64_t base = base_out(i, ch);
     // the tile leaves LDS in batches of 4 register slots, each batch stored before the next is
     // read (keeps the register budget)
     if (rout >= 4) {
@@ -342,7 +565,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
         if (st_lane) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            T* p = lane_at(Y + base + hot.st_hm[r0 + q], sto);
+            T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + q]), sto);
             *p = use_beta ? scale_add(t[q], *p, beta) : t[q];
           }
         }
@@ -350,17 +573,17 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       }
     } else {
       T t[4];
-      TQ_BY_COUNT(rout, t[r] = buf[sta ^ hot.st_ha[r]]);
+      TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ hot.st_ha[r]]);
       if (st_lane) {
-        TQ_BY_COUNT(rout, {
-          T* p = lane_at(Y + base + hot.st_hm[r], sto);
+        TQ_BY_COUNT(4, rout, {
+          T* p = lane_at(Y + uniform(base + hot.st_hm[r]), sto);
           *p = use_beta ? scale_add(t[r], *p, beta) : t[r];
         });
       }
     }
     __syncthreads();  // every wave has read the tile
     if (ch == lb) TQ_TS(5);
-    if (more) TQ_BY_COUNT(rin, buf[lda ^ hot.ld_ha[r]] = reg[r]);
+    if (more) fill(i + 1, nxt);
     __syncthreads();
   }
 #ifdef TQ_S2_TIMING

@@ -253,7 +253,8 @@ def linear_path(net: Network, order: Optional[Sequence[int]] = None,
     return path + p, root
 
 
-def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int]):
+def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int], strict: bool = False):
+    """strict: absorb in the order hint's order (connected tensors first), no size rule."""
     size = st.net.size
     remaining = set(ids)
     first = min(remaining, key=lambda t: rank[t])
@@ -264,6 +265,8 @@ def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int]):
         cand = st.neighbours(cur) & remaining
         if not cand:
             nxt = min(remaining, key=lambda t: rank[t])
+        elif strict:
+            nxt = min(cand, key=lambda t: rank[t])
         else:
             nxt = min(cand, key=lambda t: (size(st.result(cur, t)), rank[t]))
         remaining.discard(nxt)
@@ -274,9 +277,10 @@ def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int]):
 
 def partition_path(net: Network, groups: Sequence[Sequence[int]],
                    orders: Optional[Sequence[Sequence[int]]] = None,
-                   pre: Sequence[Tuple[int, int]] = ()) -> List[Tuple[int, int]]:
+                   pre: Sequence[Tuple[int, int]] = (), strict: bool = False) -> List[Tuple[int, int]]:
     """Sweep each group with linear_path, then contract the group results left to right.
-    `pre` pairs (original ids, both in one group) are contracted before the sweeps."""
+    `pre` pairs (original ids, both in one group) are contracted before the sweeps; `strict`
+    follows each order hint exactly (see _linear_on_state)."""
     st = _State(net)
     path, find = _apply_pre(st, pre)
     roots = []
@@ -284,7 +288,7 @@ def partition_path(net: Network, groups: Sequence[Sequence[int]],
         order = orders[g] if orders is not None else list(grp)
         rank0 = {t: k for k, t in enumerate(order)}
         ids, rank = _alias_group(list(grp), find, rank0)
-        p, root = _linear_on_state(st, ids, rank)
+        p, root = _linear_on_state(st, ids, rank, strict)
         path += p
         roots.append(root)
     cur = roots[0]
@@ -304,6 +308,12 @@ class PathInfo:
     slice_flops: float = 0.0  # per-slice part
     n_slices: int = 1
     est_seconds: float = 0.0  # roofline estimate of a full execute on one MI355X
+    t_once: float = 0.0       # its slice-invariant part (replicated on every rank)
+    t_slice: float = 0.0      # its per-slice part (one slice)
+
+    def est_ranks(self, world: int) -> float:
+        """Estimate of one rank's share when the slices are split over `world` ranks."""
+        return self.t_once + self.t_slice * -(-self.n_slices // max(1, world))
 
 
 # roofline constants for the cost model (MI355X: ~5 TB/s achievable HBM, ~110 TF/s sustained
@@ -343,7 +353,7 @@ def path_info(net: Network, path: Sequence[Tuple[int, int]], removed: Iterable[i
         steps.append((i, j, st.live[k], macs))
     if len(st.live) != 1:
         raise ValueError("path does not contract the network to one tensor")
-    return PathInfo(once + per * n_sl, mx, steps, once, per, n_sl, t_once + t_per * n_sl)
+    return PathInfo(once + per * n_sl, mx, steps, once, per, n_sl, t_once + t_per * n_sl, t_once, t_per)
 
 
 def validate_path(n_terms: int, path: Sequence[Tuple[int, int]]) -> None:
@@ -363,7 +373,9 @@ def validate_path(n_terms: int, path: Sequence[Tuple[int, int]]) -> None:
 def choose_slices(net: Network, path: Sequence[Tuple[int, int]], n_modes: int,
                   candidates: Optional[Sequence[int]] = None) -> List[int]:
     """Greedy index slicing: repeatedly fix the contracted mode whose removal minimises the
-    roofline time of an execute = hoisted slice-invariant steps + slices x per-slice steps.
+    roofline time of an execute = hoisted slice-invariant steps + slices x per-slice steps, on
+    one GPU plus on one rank of an 8-GPU split (the hoisted part is replicated on every rank, so
+    among equally cheap single-GPU choices the one with the smaller hoisted part wins).
     Output modes are never sliced."""
     outset = set(net.out)
     if candidates is None:
@@ -375,7 +387,7 @@ def choose_slices(net: Network, path: Sequence[Tuple[int, int]], n_modes: int,
             if m in chosen or m in outset:
                 continue
             info = path_info(net, path, chosen + [m])
-            key = (info.est_seconds, info.max_size, m)
+            key = (info.est_seconds + info.est_ranks(8), info.max_size, m)
             if best is None or key < best[0]:
                 best = (key, m)
         if best is None:

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-2 GPU session 15: diamond-tile sweep order for cut brick walls (C3/C4), slice choice
+# weighing the 8-rank estimate; parity, rank projection, bench, kernarg placement experiment.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+scripts/gpu_check.sh \
+  "ctests 400 python -u -m pytest tests/test_contract_gpu.py tests/test_fullsize_gpu.py tests/test_golden_gpu.py tests/test_distributed_gpu.py -m gpu -q -rf --timeout 200 --timeout-method thread" \
+  "ranksim 200 python scripts/rank_sim.py C4" \
+  "s2t 200 env TNEQHIP_LIB=$PWD/quantum_circuits_symmetry_breaking_based_on_tneq-qc_amd/lib/libtneqhip_s2t.so python scripts/sweep_timing.py C4" \
+  "s2tk 200 env HIP_FORCE_DEV_KERNARG=1 TNEQHIP_LIB=$PWD/quantum_circuits_symmetry_breaking_based_on_tneq-qc_amd/lib/libtneqhip_s2t.so python scripts/sweep_timing.py C4" \
+  "bench 300 python bench.py --no-c5"

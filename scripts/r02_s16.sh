@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-2 GPU session 16: SWEEP2 register-block passes (runs of square gates applied in
+# registers, one LDS round trip and one barrier per run); parity, timing, A/B against
+# TQ_S2_BLOCKS=0, bench.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+scripts/gpu_check.sh \
+  "ctests 400 python -u -m pytest tests/test_contract_gpu.py tests/test_fullsize_gpu.py tests/test_kernels_gpu.py tests/test_golden_gpu.py tests/test_autograd_gpu.py -m gpu -q -rf --timeout 200 --timeout-method thread" \
+  "ranksim 200 python scripts/rank_sim.py C4" \
+  "ranksim0 200 env TQ_S2_BLOCKS=0 python scripts/rank_sim.py C4" \
+  "s2t 200 env TNEQHIP_LIB=$PWD/quantum_circuits_symmetry_breaking_based_on_tneq-qc_amd/lib/libtneqhip_s2t.so python scripts/sweep_timing.py C4" \
+  "bench 300 python bench.py --no-c5"
