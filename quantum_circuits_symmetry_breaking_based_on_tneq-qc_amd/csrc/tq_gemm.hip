@@ -16,6 +16,7 @@
 //  * XCD-aware tile order: tiles that share an A row panel are dealt to the same XCD.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "tq_common.h"
 
@@ -549,6 +550,243 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
   else store(std::false_type{});
 }
 
+// ---------------------------------------------------------------------------------------------
+// FP64 fast path: float64 / complex128 with both operands K-outer (A stored K x M, B K x N) — the
+// same layout as the complex64 fast path, for the fp64 workloads (the symmetry-breaking ansatz,
+// BASELINE config 5) — on v_mfma_f64_16x16x4_f64.
+//
+//  * operands reach LDS by LDS-DMA (global_load_lds_dwordx4: one wave-instruction = 1 KiB of one
+//    k-row), in an NS-stage ring with NS - 1 K-tiles in flight, one counted vmcnt wait and one
+//    raw s_barrier per K-tile (as the complex64 kernel above);
+//  * fragments: lane l reads element (k = kk + l/16, m = .. + l%16) — 16 consecutive elements
+//    of one k-row per 16 lanes: one ds_read_b64 (f64) / ds_read_b128 (re, im of a complex128)
+//    per MFMA operand, conflict-free; the next k-step's fragments are read under this one's MFMAs;
+//  * complex128: Gauss 3M (3 real MFMAs per complex k-step, default) or 4M (TQ_GEMM_3M=0);
+//  * C/D of the f64 MFMA: col = lane%16, row = lane/16 + 4 r (cdna_hip_programming.md §3);
+//  * split-K over the grid with the deterministic slab reduce, bijective XCD remap.
+namespace fast64 {
+template <int WMW_, int WNW_, int TI_, int TJ_, int BK_, int NS_, int ESZ_> struct Tile {
+  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_, BK = BK_, NS = NS_, ESZ = ESZ_;
+  static constexpr int NW = WMW * WNW, NT = 64 * NW;
+  static constexpr int WM = 16 * TI, WN = 16 * TJ;
+  static constexpr int BM = WMW * WM, BN = WNW * WN;
+  static constexpr int A_BYTES = BK * BM * ESZ, B_BYTES = BK * BN * ESZ, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_ROW_PIECES = BM * ESZ / 1024, B_ROW_PIECES = BN * ESZ / 1024;
+  static constexpr int A_PIECES_PER_WAVE = BK * A_ROW_PIECES / NW;
+  static constexpr int B_PIECES_PER_WAVE = BK * B_ROW_PIECES / NW;
+  static constexpr int NDMA = A_PIECES_PER_WAVE + B_PIECES_PER_WAVE;
+  static_assert(BM * ESZ % 1024 == 0 && BN * ESZ % 1024 == 0, "1-KiB row pieces");
+  static_assert(BK * A_ROW_PIECES % NW == 0 && BK * B_ROW_PIECES % NW == 0, "piece split");
+  static_assert(BK % 4 == 0, "MFMA k-step");
+};
+// float64: 8 waves of 64 x 32 (4 x 2 MFMA tiles, 64 accumulator VGPRs), block 128 x 128,
+// BK 16, 3 x 32 KiB stages
+using TileF64 = Tile<2, 4, 4, 2, 16, 3, 8>;
+// complex128: 8 waves of 32 x 32 (2 x 2 tiles x 3 (3M) accumulator sets = 96 VGPRs), block
+// 64 x 128, BK 8, 3 x 24 KiB stages
+using TileC128 = Tile<2, 4, 2, 2, 8, 3, 16>;
+}
+
+struct FastArgs64 {
+  const double* A;  // K x M elements (lda elements between k-rows)
+  const double* B;  // K x N elements
+  double* C;        // output (ldc) or split-K slabs
+  double* W;
+  int64_t lda, ldb, ldc, sA, sB, sC, M, N;
+  int64_t kchunk;
+  int mt, nt, splits, batch;
+  double beta;
+};
+
+template <bool CPLX, bool G3M, typename TL>
+__global__ void __launch_bounds__(TL::NT, 1) gemm_f64_kouter_kernel(FastArgs64 g) {
+  using namespace fast64;
+  constexpr int BM = TL::BM, BN = TL::BN, WMW = TL::WMW, TI = TL::TI, TJ = TL::TJ, BK = TL::BK;
+  constexpr int STAGE = TL::STAGE, A_BYTES = TL::A_BYTES, NSTAGE = TL::NS, ESZ = TL::ESZ;
+  constexpr int EW = CPLX ? 2 : 1;
+  constexpr int NACC = CPLX ? (G3M ? 3 : 2) : 1;
+  static_assert(ESZ == 8 * EW, "element size");
+  __shared__ __attribute__((aligned(16))) char lds[NSTAGE * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % WMW, wn = wid / WMW;
+  const int nblk = gridDim.x;
+  int L = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, xcd = L % 8, idx = L / 8;
+    if (nblk >= 8) L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int ntile = g.mt * g.nt;
+  const int tile = L % ntile;
+  const int split = (L / ntile) % g.splits;
+  const int b = L / (ntile * g.splits);
+  const int tm = tile / g.nt, tn = tile % g.nt;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * g.kchunk;
+  const int nkt = (int)(g.kchunk / BK);
+  const char* A = reinterpret_cast<const char*>(g.A + ((int64_t)b * g.sA + kbeg * g.lda + m0) * EW);
+  const char* B = reinterpret_cast<const char*>(g.B + ((int64_t)b * g.sB + kbeg * g.ldb + n0) * EW);
+  const int64_t lda_b = g.lda * ESZ, ldb_b = g.ldb * ESZ;
+
+  const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  auto glds16 = [&](const char* gsrc, unsigned lds_off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + lds_off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+  };
+  auto issue = [&](int t, int stage) {
+    const unsigned sbase = stage * STAGE;
+#pragma unroll
+    for (int q = 0; q < TL::A_PIECES_PER_WAVE; ++q) {
+      const int p = wid * TL::A_PIECES_PER_WAVE + q;
+      const int kr = p / TL::A_ROW_PIECES, mp = p % TL::A_ROW_PIECES;
+      glds16(A + ((int64_t)t * BK + kr) * lda_b + mp * 1024 + lane * 16, sbase + p * 1024);
+    }
+#pragma unroll
+    for (int q = 0; q < TL::B_PIECES_PER_WAVE; ++q) {
+      const int p = wid * TL::B_PIECES_PER_WAVE + q;
+      const int kr = p / TL::B_ROW_PIECES, np = p % TL::B_ROW_PIECES;
+      glds16(B + ((int64_t)t * BK + kr) * ldb_b + np * 1024 + lane * 16, sbase + A_BYTES + p * 1024);
+    }
+  };
+
+  f64x4 acc[NACC][TI][TJ];
+#pragma unroll
+  for (int x = 0; x < NACC; ++x)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[x][i][j][r] = 0.0;
+
+  const int fr = lane & 15, fk = lane >> 4;
+  const int a_off = (fk * BM + wm * TL::WM + fr) * ESZ;
+  const int b_off = A_BYTES + (fk * BN + wn * TL::WN + fr) * ESZ;
+  using Frag = typename std::conditional<CPLX, double2, double>::type;
+
+  for (int p = 0; p < NSTAGE - 1 && p < nkt; ++p) issue(p, p);
+  for (int t = 0; t < nkt; ++t) {
+    if (NSTAGE > 2 && t + 1 < nkt) vm_wait<TL::NDMA * (NSTAGE > 2 ? NSTAGE - 2 : 0)>();
+    else vm_wait<0>();
+    asm volatile("s_barrier" ::: "memory");
+    if (t + NSTAGE - 1 < nkt) issue(t + NSTAGE - 1, (t + NSTAGE - 1) % NSTAGE);
+    const char* s = lds + (t % NSTAGE) * STAGE;
+    Frag a[TI], bb[TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const Frag*>(s + a_off + i * 16 * ESZ);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) bb[j] = *reinterpret_cast<const Frag*>(s + b_off + j * 16 * ESZ);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      Frag na[TI], nb[TJ];
+      if (kk + 4 < BK) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+          na[i] = *reinterpret_cast<const Frag*>(s + a_off + ((kk + 4) * BM + i * 16) * ESZ);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          nb[j] = *reinterpret_cast<const Frag*>(s + b_off + ((kk + 4) * BN + j * 16) * ESZ);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!CPLX) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[0][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[0][i][j], 0, 0, 0);
+      } else if constexpr (G3M) {
+        double sa[TI], sb[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) sa[i] = a[i].x + a[i].y;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) sb[j] = bb[j].x + bb[j].y;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].x, bb[j].x, acc[0][i][j], 0, 0, 0);
+            acc[1][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].y, bb[j].y, acc[1][i][j], 0, 0, 0);
+            acc[2][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[i], sb[j], acc[2][i][j], 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].x, bb[j].x, acc[0][i][j], 0, 0, 0);
+            acc[1][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].x, bb[j].y, acc[1][i][j], 0, 0, 0);
+          }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[i].y, bb[j].y, acc[0][i][j], 0, 0, 0);
+            acc[1][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i].y, bb[j].x, acc[1][i][j], 0, 0, 0);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kk + 4 < BK) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) a[i] = na[i];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bb[j] = nb[j];
+      }
+    }
+  }
+
+  const bool partial = g.splits > 1;
+  double* Cout = partial ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * EW : g.C + (int64_t)b * g.sC * EW;
+  const int64_t ldo = partial ? g.N : g.ldc;
+  const double beta = partial ? 0.0 : g.beta;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + wm * TL::WM + i * 16 + (lane >> 4) + 4 * r;
+        const int64_t gn = n0 + wn * TL::WN + j * 16 + (lane & 15);
+        double* p = Cout + (gm * ldo + gn) * EW;
+        if constexpr (!CPLX) {
+          const double v = acc[0][i][j][r];
+          p[0] = beta != 0.0 ? v + beta * p[0] : v;
+        } else {
+          double2 v;
+          if constexpr (G3M) {
+            const double p1 = acc[0][i][j][r], p2 = acc[1][i][j][r];
+            v = make_double2(p1 - p2, acc[2][i][j][r] - p1 - p2);
+          } else {
+            v = make_double2(acc[0][i][j][r], acc[1][i][j][r]);
+          }
+          if (beta != 0.0) {
+            const double2 o = *reinterpret_cast<const double2*>(p);
+            v.x += beta * o.x;
+            v.y += beta * o.y;
+          }
+          *reinterpret_cast<double2*>(p) = v;
+        }
+      }
+}
+
+template <typename TL>
+int fast_f64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  constexpr int BK = TL::BK;
+  if (!(transA == 1 && transB == 0)) return 0;
+  if (M % TL::BM || N % TL::BN || K % BK || K == 0) return 0;
+  const int64_t tiles = (M / TL::BM) * (N / TL::BN) * batch;
+  int s = 1;
+  while (tiles * s * 2 <= 256 && K % ((int64_t)s * 2 * BK) == 0 && K / ((int64_t)s * 2 * BK) >= 32) s *= 2;
+  if (tiles * s > INT32_MAX) return 0;
+  return s;
+}
+int fast_f64_splits(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (dtype == TQ_F64) return fast_f64_splits_t<fast64::TileF64>(transA, transB, M, N, K, batch);
+  if (dtype == TQ_C128) return fast_f64_splits_t<fast64::TileC128>(transA, transB, M, N, K, batch);
+  return 0;
+}
+
 // eligibility and split choice of the fast path (shared by launch and workspace sizing)
 template <typename TL>
 int fast_c64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
@@ -635,6 +873,43 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       return TQ_OK;
     }
   }
+  if constexpr (sizeof(R) == 8) {
+    const int dt = CPLX ? TQ_C128 : TQ_F64;
+    const int fs = fast_f64_splits(dt, transA, transB, M, N, K, batch);
+    const bool al = ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+                    (CPLX || (lda % 2 == 0 && ldb % 2 == 0 && (batch == 1 || (sA % 2 == 0 && sB % 2 == 0))));
+    const size_t need = (size_t)fs * batch * M * N * EW * sizeof(double);
+    if (fs > 0 && al && (fs == 1 || (W != nullptr && wsb >= need)) && !fast_disabled()) {
+      FastArgs64 f{};
+      f.A = (const double*)A; f.B = (const double*)B; f.C = (double*)C; f.W = (double*)W;
+      f.lda = lda; f.ldb = ldb; f.ldc = ldc; f.sA = sA; f.sB = sB; f.sC = sC; f.M = M; f.N = N;
+      f.kchunk = K / fs;
+      f.splits = fs; f.batch = (int)batch; f.beta = beta;
+      auto go = [&](auto tl, auto g3c) {
+        using TL = decltype(tl);
+        f.mt = (int)(M / TL::BM);
+        f.nt = (int)(N / TL::BN);
+        const int64_t nblk = (int64_t)f.mt * f.nt * fs * batch;
+        hipLaunchKernelGGL((gemm_f64_kouter_kernel<CPLX, decltype(g3c)::value, TL>), dim3((unsigned)nblk),
+                           dim3(TL::NT), 0, stream, f);
+      };
+      if constexpr (CPLX) {
+        if (gemm_3m()) go(fast64::TileC128{}, std::true_type{});
+        else go(fast64::TileC128{}, std::false_type{});
+      } else {
+        go(fast64::TileF64{}, std::false_type{});
+      }
+      TQ_HIP(hipGetLastError());
+      if (fs > 1) {
+        const int64_t total = batch * M * N * EW;
+        const int blocks = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 4096);
+        hipLaunchKernelGGL((splitk_reduce_kernel<double>), dim3(blocks), dim3(kThreads), 0, stream,
+                           (const double*)W, (double*)C, M, N, ldc, sC, batch, fs, EW, beta);
+        TQ_HIP(hipGetLastError());
+      }
+      return TQ_OK;
+    }
+  }
   GemmArgs g{};
   g.A = A; g.B = B; g.C = C; g.W = W;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
@@ -705,6 +980,7 @@ size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch)
   const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   int s = choose_splits(tiles, K, (int)bk);
   if (dtype == TQ_C64) s = std::max(s, fast_c64_splits(1, 0, M, N, K, batch));
+  if (dtype == TQ_F64 || dtype == TQ_C128) s = std::max(s, fast_f64_splits(dtype, 1, 0, M, N, K, batch));
   if (s <= 1) return 0;
   return (size_t)s * batch * M * N * dtype_size(dtype);
 }

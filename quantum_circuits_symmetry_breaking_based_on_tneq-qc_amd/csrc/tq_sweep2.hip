@@ -61,7 +61,9 @@ static_assert(kLut == 64, "lut layout shared with S2Desc::lut");
 #ifdef TQ_S2_TIMING
 // development instrumentation (built only with -DTQ_S2_TIMING): workgroup 0 of every op records
 // wall-clock stamps (100 MHz) at its phase boundaries
-constexpr int kTsMax = 4096, kTsPh = 9;
+// record: [0..6] phase stamps, [7] blocks|chunks, [8] first chunk's gate clocks,
+// [9..24] clock at the end of each pass of the first chunk, [25..40] pass kind (B<<16|K<<8|N)
+constexpr int kTsMax = 2048, kTsPh = 41;
 __device__ unsigned long long g_s2_ts[kTsMax][kTsPh];
 __device__ unsigned int g_s2_seq;
 #define TQ_TS(ph) do { if (ts_rec && threadIdx.x == 0) g_s2_ts[ts_idx][ph] = wall_clock64(); } while (0)
@@ -341,6 +343,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   __syncthreads();
   const unsigned ts_idx = ts_slot;
   TQ_TS(0);
+  if (ts_rec && threadIdx.x == 0)
+    for (int q = 9; q < kTsPh; ++q) g_s2_ts[ts_idx][q] = 0;
 #endif
   // ---- the descriptor is staged in the (not yet used) tile buffer by one coalesced pass; the
   // tables below are built from that copy (no chains of dependent scalar loads)
@@ -546,6 +550,13 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       }
       else block_pass<T, 3>(buf, cf, pm, lut + g * kLut, logC);
       __syncthreads();
+#ifdef TQ_S2_TIMING
+      if (ch == lb && ts_rec && threadIdx.x == 0 && p < 16) {
+        g_s2_ts[ts_idx][9 + p] = clock64() - clk0;
+        g_s2_ts[ts_idx][25 + p] = ((unsigned long long)bk << 16) | (gmeta[g * kGm + kGmK] << 8) |
+                                  gmeta[g * kGm + kGmN] | ((unsigned long long)pm[kS2PmCount] << 24);
+      }
+#endif
     }
     if (ch == lb) TQ_TS(4);
 #ifdef TQ_S2_TIMING

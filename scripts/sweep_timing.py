@@ -15,7 +15,8 @@ L = _lib.lib()
 f = L.tq_debug_sweep2_timing
 f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 f.restype = ctypes.c_int
-buf = (ctypes.c_ulonglong * (4096 * 9))()
+NREC, W = 2048, 41
+buf = (ctypes.c_ulonglong * (NREC * W))()
 task = config_task(sys.argv[1] if len(sys.argv) > 1 else "C4")
 expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
 dev = torch.device("cuda:0")
@@ -24,11 +25,11 @@ out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
 for _ in range(3):
     expr(*ops, out=out, slice_range=(0, 1, 1))
 torch.cuda.synchronize()
-f(buf, 4096)  # drain
+f(buf, NREC)  # drain
 expr(*ops, out=out, slice_range=(0, 1, 1))
 torch.cuda.synchronize()
-n = f(buf, 4096)
-a = np.frombuffer(buf, dtype=np.uint64, count=n * 9).reshape(n, 9).astype(np.int64)
+n = f(buf, NREC)
+a = np.frombuffer(buf, dtype=np.uint64, count=n * W).reshape(n, W).astype(np.int64)
 a = a[np.argsort(a[:, 0])]
 t0 = a[0, 0]
 names = ["desc", "tables", "chunk0_in", "gates0", "store0", "rest+drain"]
@@ -40,3 +41,18 @@ for r in a:
     print(f"start {(r[0]-t0)/100:8.2f} end {(r[6]-t0)/100:8.2f} | " + " ".join(f"{x:6.2f}" for x in ph)
           + f" | wgs {int(r[7]) >> 32} chunks {int(r[7]) & 0xffffffff} | gate clk {r[8] / max(ph[3], 1e-3) / 1e3:6.0f} MHz")
 print("sum per phase:", json.dumps(dict(zip(names, np.round(tot, 1).tolist()))))
+# per-pass clocks of the first chunk (shader clock), grouped by pass kind
+kinds = {}
+for r in a:
+    prev = 0
+    for p in range(16):
+        t = int(r[9 + p])
+        if t == 0:
+            break
+        k = int(r[25 + p])
+        key = (f"B{(k >> 16) & 0xff}x{k >> 24}" if (k >> 16) & 0xff else f"{(k >> 8) & 0xff}x{k & 0xff}")
+        kinds.setdefault(key, []).append(t - prev)
+        prev = t
+print("per-pass clocks (first chunk, WG0): kind -> (count, median, mean)")
+for k, v in sorted(kinds.items(), key=lambda kv: -len(kv[1])):
+    print(f"  {k:8s} {len(v):4d} {int(np.median(v)):7d} {int(np.mean(v)):7d}")

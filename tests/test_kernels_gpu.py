@@ -151,6 +151,25 @@ def test_gemm_c64_kouter_fast_path(T, dev, M, N, K, B, beta):
     assert err < TOL["complex64"], (M, N, K, B, err)
 
 
+@pytest.mark.parametrize("dt", ["float64", "complex128"])
+@pytest.mark.parametrize("M,N,K,B,beta", [(128, 128, 32, 1, 0.0), (256, 256, 48, 3, 0.0),
+                                           (512, 256, 4096, 1, 1.0), (1024, 1024, 8192, 1, 0.0),
+                                           (256, 256, 2048, 2, 0.5), (384, 384, 1024, 1, 0.0)])
+def test_gemm_f64_kouter_fast_path(T, dev, dt, M, N, K, B, beta):
+    """float64 / complex128 with A stored K x M and B stored K x N: the LDS-DMA v_mfma_f64 kernel
+    (3-stage ring, split-K slabs, Gauss 3M for complex128) — tile-grid shapes, batched, beta."""
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(11)
+    a = _rand(rng, (B, K, M), dt)
+    b = _rand(rng, (B, K, N), dt)
+    c0 = _rand(rng, (B, M, N), dt)
+    cd = _to(T, dev, c0)
+    ops.gemm(_to(T, dev, a), _to(T, dev, b), True, False, out=cd, beta=beta)
+    ref = np.matmul(np.swapaxes(a, 1, 2), b) + beta * c0
+    err = np.abs(cd.cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err < TOL[dt], (dt, M, N, K, B, err)
+
+
 def test_gemm_c64_bench_shape(T, dev):
     """The exact boundary GEMM of the C4 bench (M = N = 1024, K = 65536 per slice, complex64, both
     operands K-outer; the library splits K 4 ways over the workspace, as in the plan) on random
