@@ -35,6 +35,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, f32-in MFMA
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA peak (no sparsity) at 2.4 GHz
+PEAK_CLOCK_GHZ = 2.4
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 N_OPEN_CPU = 20                 # open outputs in the CPU-baseline sample (one slice: ~5-15 s of numpy)
 
@@ -178,6 +180,20 @@ def c5_train(dev, with_cpu: bool = True, steps: int = 5, warmup: int = 2):
     return r
 
 
+def alt_f32(args):
+    """The same headline with the boundary GEMM on the f32 MFMA kernel (TQ_GEMM_BF16=0, the
+    library reads it once per process: a child process, started without exec)."""
+    import subprocess
+    env = dict(os.environ, TQ_GEMM_BF16="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", args.config, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
+            "gemm": "v_mfma_f32_32x32x2_f32 (TQ_GEMM_BF16=0)", "roofline": d["roofline"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,6 +202,8 @@ def main():
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 training-step line")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip the f32-MFMA GEMM headline (TQ_GEMM_BF16=0, a child process)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -257,16 +275,33 @@ def main():
     plan.profile(None)
 
     n_amp = task.n_amplitudes
-    g3m = bool(_lib.lib().tq_library_query(b"gemm_3m") == 1)
+    L = _lib.lib()
+    g3m = bool(L.tq_library_query(b"gemm_3m") == 1)
+    bf16 = bool(L.tq_library_query(b"gemm_bf16") == 1)
     value = n_amp * args.steps / dt
     nl = max(1, gemm["launches"])
     avg_gemm_s = gemm["ms"] / 1e3 / nl
     alg_flops = gemm["flops"] / nl                      # 8*M*N*K complex GEMM flops per launch
-    exe_flops = alg_flops * (0.75 if g3m else 1.0)      # MFMA work executed: 3M = 6*M*N*K, 4M = 8*M*N*K
+    # MFMA work executed per launch: bf16 split = 4 real products x 6 term products = 48*M*N*K;
+    # f32 3M = 6*M*N*K, f32 4M = 8*M*N*K
+    exe_flops = alg_flops * (6.0 if bf16 else (0.75 if g3m else 1.0))
+    peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     achieved = exe_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     alg_rate = alg_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
-    pmc_t = _profile_json("pmc_gemm.json", args.config)
-    pmc_b = _profile_json("pmc_gemm_busy_r02.json", args.config)
+    if bf16:
+        pmc_b = _profile_json("pmc_gemm_bf16_r02.json", args.config)
+        pmc_t = pmc_b
+        kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_bf16: every f32 operand split exactly into "
+                 "3 bf16 terms, 6 term products kept, f32 accumulation; 4 real products per complex product)")
+        exe_def = "executed bf16 MFMA flops per launch (4 real products x 6 term products = 48*M*N*K) / avg launch time"
+    else:
+        pmc_t = _profile_json("pmc_gemm.json", args.config)
+        pmc_b = _profile_json("pmc_gemm_busy_r02.json", args.config)
+        kdesc = ("boundary GEMM (complex64, LDS-DMA fed v_mfma_f32_32x32x2_f32, "
+                 + ("Gauss 3M: 3 real f32 MFMA GEMMs per complex GEMM" if g3m
+                    else "4 real f32 MFMA GEMMs per complex GEMM") + ")")
+        exe_def = "executed MFMA flops per launch (3M: 6*M*N*K, 4M: 8*M*N*K real) / avg launch time"
+    clk = (pmc_b or {}).get("effective_clock_GHz")
     apply_ = kinds["APPLY"]
     sweep_ = kinds["SWEEP"]
     perm_ = kinds["PERMUTE"]
@@ -300,15 +335,14 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": ("boundary GEMM (complex64, LDS-DMA fed v_mfma_f32_32x32x2_f32, "
-                       + ("Gauss 3M: 3 real f32 MFMA GEMMs per complex GEMM" if g3m
-                          else "4 real f32 MFMA GEMMs per complex GEMM") + ")"),
+            "kernel": kdesc,
             "achieved": achieved,
-            "peak": PEAK_FP32_MFMA_TFLOPS,
+            "peak": peak,
             "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
-            "achieved_definition": ("executed MFMA flops per launch (3M: 6*M*N*K, 4M: 8*M*N*K real) / "
-                                    "avg launch time (HIP events on the GEMM's stream, eager pass)"),
+            "frac": achieved / peak,
+            "achieved_definition": exe_def + " (HIP events on the GEMM's stream, eager pass)",
+            "effective_clock_GHz_pmc": clk,
+            "frac_at_measured_clock": (achieved / (peak * clk / PEAK_CLOCK_GHZ)) if clk else None,
             "algorithmic_tflops": alg_rate,
             "algorithmic_definition": "complex-GEMM flops 8*M*N*K per launch / avg launch time",
             "mfma_busy_pmc": (pmc_b or {}).get("mfma_busy_frac"),
@@ -347,6 +381,11 @@ def main():
             res["cpu_baseline"] = cpu_baseline(args.config)
         except Exception as e:  # the baseline must never hide the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
+    if world == 1 and rank == 0 and bf16 and not args.no_alt:
+        try:
+            res["alt_f32_mfma"] = alt_f32(args)
+        except Exception as e:  # the alternate line must never hide the headline
+            res["alt_f32_mfma"] = {"error": repr(e)}
     if world == 1 and rank == 0 and not args.no_c5:
         try:
             res["c5_train"] = c5_train(dev, with_cpu=not args.no_cpu_baseline)

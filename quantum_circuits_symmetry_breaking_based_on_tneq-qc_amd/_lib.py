@@ -19,7 +19,7 @@ TQ_OK, TQ_ERR_INVALID, TQ_ERR_HIP, TQ_ERR_ALLOC, TQ_ERR_UNSUPPORTED = 0, -1, -2,
 
 # every symbol the header declares (tests check the .so exports all of them)
 EXPORTED = (
-    "tq_version", "tq_last_error", "tq_device_synchronize", "tq_library_query", "tq_permute",
+    "tq_version", "tq_last_error", "tq_device_synchronize", "tq_library_query", "tq_library_set", "tq_permute",
     "tq_gemm_batched",
     "tq_gemm_workspace_size", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
     "tq_plan_create", "tq_plan_query", "tq_plan_set", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
@@ -48,6 +48,7 @@ _SIGS = {
     "tq_last_error": (_c.c_int, [_c.c_char_p, _c.c_size_t]),
     "tq_device_synchronize": (_c.c_int, []),
     "tq_library_query": (_c.c_int64, [_c.c_char_p]),
+    "tq_library_set": (_c.c_int, [_c.c_char_p, _c.c_int64]),
     "tq_permute": (_c.c_int, [_c.c_int, _c.c_int, _i64p, _i64p, _vp, _vp, _c.c_double, _vp]),
     "tq_gemm_batched": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64,
                                    _c.c_int64, _vp, _c.c_int64, _c.c_int64, _vp, _c.c_int64,

@@ -17,6 +17,8 @@ const std::string& last_error() { return g_last_error; }
 
 namespace tq {
 bool gemm_3m();
+bool gemm_bf16();
+bool gemm_configure(const char* key, int64_t v);
 bool graphs_enabled();
 bool sweeps_enabled_global();
 }
@@ -25,10 +27,18 @@ extern "C" int64_t tq_library_query(const char* key) {
   if (!key) return -1;
   const std::string k(key);
   if (k == "gemm_3m") return tq::gemm_3m() ? 1 : 0;
+  if (k == "gemm_bf16") return tq::gemm_bf16() ? 1 : 0;
   if (k == "graphs") return tq::graphs_enabled() ? 1 : 0;
   if (k == "sweep") return tq::sweeps_enabled_global() ? 1 : 0;
 
   return -1;
+}
+
+extern "C" int tq_library_set(const char* key, int64_t value) {
+  if (!key) return TQ_ERR_INVALID;
+  if (tq::gemm_configure(key, value)) return TQ_OK;
+  tq::set_error(std::string("tq_library_set: unknown key ") + key);
+  return TQ_ERR_INVALID;
 }
 
 // development only (not in the public header): drains the sweep2 phase stamps of a library

@@ -15,6 +15,8 @@
 //    output tile count alone cannot fill 256 CUs.
 //  * XCD-aware tile order: tiles that share an A row panel are dealt to the same XCD.
 #include <algorithm>
+#include <atomic>
+#include <string>
 #include <cstdlib>
 #include <type_traits>
 
@@ -25,14 +27,25 @@ namespace tq {
 // The fast path computes complex products with Gauss's 3 real multiplications (default; the C4
 // amplitudes stay within 4.0e-6 of complex128, vs 2.7e-6 for the 4-multiplication product);
 // TQ_GEMM_3M=0 selects the 4-multiplication kernel.
-bool gemm_3m() {
-  static const int v = [] {
-    const char* e = getenv("TQ_GEMM_3M");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v != 0;
+static int env_flag(const char* name) {
+  const char* e = getenv(name);
+  return (e && e[0] == '0') ? 0 : 1;
 }
-
+static std::atomic<int> g_gemm_3m{env_flag("TQ_GEMM_3M")};
+static std::atomic<int> g_gemm_bf16{env_flag("TQ_GEMM_BF16")};
+bool gemm_3m() { return g_gemm_3m.load(std::memory_order_relaxed) != 0; }
+// The complex64 K-outer fast path runs on the bf16 matrix cores with an exact 3-term split of
+// every f32 operand (gemm_c64_kouter_bf16_kernel, f32 accuracy); TQ_GEMM_BF16=0 (or
+// tq_library_set("gemm_bf16", 0)) selects the f32-MFMA kernel.
+bool gemm_bf16() { return g_gemm_bf16.load(std::memory_order_relaxed) != 0; }
+// runtime switch (tq_library_set): affects launches issued after the call (plans replaying a
+// captured hipGraph keep the kernels they captured)
+bool gemm_configure(const char* key, int64_t v) {
+  const std::string k(key);
+  if (k == "gemm_3m") { g_gemm_3m = v ? 1 : 0; return true; }
+  if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
+  return false;
+}
 
 namespace {
 
@@ -551,6 +564,261 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
 }
 
 // ---------------------------------------------------------------------------------------------
+// complex64 on the bf16 matrix cores with f32 accuracy (default K-outer complex64 fast path;
+// TQ_GEMM_BF16=0 selects the f32-MFMA kernel above).
+//
+// Split: every f32 value x is split EXACTLY into three bf16 terms by truncation, h = x with the
+// low 16 bits cleared, r = x - h (exact, <= 16 significant bits), m = r truncated the same way,
+// l = r - m (exact, <= 8 significant bits, a bf16 with no rounding): x == h + m + l.  A real
+// product a*b keeps the six terms down to 2^-16 relative (hh, hm, mh, hl, lh, mm; the dropped
+// ml, lm, ll are <= 2^-24 relative, below the f32 product's own rounding), each one
+// v_mfma_f32_32x32x16_bf16 accumulating in f32.  The complex product is the 4-multiplication
+// form (Cr += Ar Br + (-Ai) Bi, Ci += Ar Bi + Ai Br; -Ai by flipping the fragment's sign bits):
+// 24 bf16 MFMAs of 32 cycles per 32 x 32 x 16 complex tile-step against 4 x 8 f32 MFMAs of 64
+// (2.67x fewer MFMA cycles).  Measured alternatives at the C4 shape (1024 x 1024 x 65536, r02):
+// this kernel 2.61-2.63 ms; the same with Gauss 3M (18 MFMAs, a third split plane re + im)
+// 2.52 ms with one wave per SIMD; split into bf16 term planes by a separate HBM pass and
+// streamed by LDS-DMA 2.35-2.7 ms + 0.32 ms per operand split (fill-bound: 18 B per element);
+// the f32-MFMA kernel 3.35 ms.  The clock runs at ~1.9 GHz under this load (PMC GRBM_GUI_ACTIVE),
+// where the 24-MFMA floor is 1.66 ms; what is left is the per-K-step barrier and in-order issue
+// (MFMA busy 62-64 %).
+//
+// Data path per K-step of 16: each thread loads KPT complex values (consecutive k of one row) of
+// A and of B straight into registers one K-step ahead of their split (two register sets, the
+// loop is unrolled by two), and splits them into the other half of a double-buffered LDS image
+// while this step's MFMAs run: 2 planes x 3 terms.  The MFMA fragment of lane (row r, k-half h)
+// is one ds_read_b128; term-plane rows are 32 B (16 k) and the two 16-B k-halves of a row are
+// swapped on every other group of 8 rows, which makes every 16-lane group of a fragment read hit
+// 16 distinct bank slots (PMC SQ_LDS_BANK_CONFLICT = 0).  One barrier per K-step.
+namespace xbf {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+template <int WMW_, int WNW_, int TI_, int TJ_> struct Tile {
+  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_;
+  static constexpr int NW = WMW * WNW, NT = 64 * NW;
+  static constexpr int WM = 32 * TI, WN = 32 * TJ, BM = WMW * WM, BN = WNW * WN, BK = 16;
+  static constexpr int SUBA = BM * 32, SUBB = BN * 32;            // bytes per term plane
+  static constexpr int BUF = 6 * (SUBA + SUBB);                   // 2 planes x 3 terms, A and B
+  // one split task per thread and operand: KPT consecutive k of one row
+  static constexpr int KPT = 16 * BM / NT;
+  static_assert(BM == BN && (KPT == 4 || KPT == 8), "task split");
+  static_assert(2 * BUF <= 160 * 1024, "LDS");
+};
+// 8 waves (two per SIMD) of 64 x 32, block 128 x 128: 2 x 48 KiB LDS, 64 accumulators per wave;
+// 4-k split tasks (ds_write_b64)
+using TileX = Tile<2, 4, 2, 1>;
+
+__device__ __forceinline__ uint32_t hi16(float x) { return __float_as_uint(x) & 0xffff0000u; }
+// pack the bf16 held in the high halves of two dwords: lo <- a, hi <- b
+__device__ __forceinline__ uint32_t pk(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
+// split N values into three packed bf16 terms (h, m, l; N/2 dwords each), exactly
+template <int N>
+__device__ __forceinline__ void splitn(const float (&v)[N], uint32_t (&h)[N / 2], uint32_t (&m)[N / 2], uint32_t (&l)[N / 2]) {
+  uint32_t hb[N], mb[N], lb[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    hb[j] = hi16(v[j]);
+    const float r = v[j] - __uint_as_float(hb[j]);
+    mb[j] = hi16(r);
+    lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
+  }
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    h[j] = pk(hb[2 * j], hb[2 * j + 1]);
+    m[j] = pk(mb[2 * j], mb[2 * j + 1]);
+    l[j] = pk(lb[2 * j], lb[2 * j + 1]);
+  }
+}
+template <int N>
+__device__ __forceinline__ void st_lds(char* p, const uint32_t (&w)[N / 2]) {
+  if constexpr (N == 8) *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  else *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+}
+
+// byte offset of (row, k-half) inside a term plane
+__device__ __forceinline__ int swz(int row, int kh) { return row * 32 + ((kh ^ ((row >> 3) & 1)) << 4); }
+__device__ __forceinline__ uint4 neg8(uint4 v) {
+  return make_uint4(v.x ^ 0x80008000u, v.y ^ 0x80008000u, v.z ^ 0x80008000u, v.w ^ 0x80008000u);
+}
+}  // namespace xbf
+
+template <typename TL>
+__global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArgs g) {
+  using namespace xbf;
+  constexpr int BM = TL::BM, BN = TL::BN, BK = TL::BK, WMW = TL::WMW, TI = TL::TI, TJ = TL::TJ;
+  constexpr int SUBA = TL::SUBA, SUBB = TL::SUBB, BUF = TL::BUF;
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % WMW, wn = wid / WMW;
+
+  const int nblk = gridDim.x;
+  int L = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, xcd = L % 8, idx = L / 8;
+    if (nblk >= 8) L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int ntile = g.mt * g.nt;
+  const int tile = L % ntile;
+  const int split = (L / ntile) % g.splits;
+  const int b = L / (ntile * g.splits);
+  const int tm = tile / g.nt, tn = tile % g.nt;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)split * g.kchunk;
+  const int nkt = (int)(g.kchunk / BK);
+
+  const float2* A = reinterpret_cast<const float2*>(g.A) + ((int64_t)b * g.sA + kbeg * g.lda + m0);
+  const float2* B = reinterpret_cast<const float2*>(g.B) + ((int64_t)b * g.sB + kbeg * g.ldb + n0);
+
+  // staging registers, two sets (K-step parity): KPT complex (k0 .. k0+KPT-1 of one row);
+  // task = thread: row = tid / (16 / KPT), k-group = tid % (16 / KPT) (a 16-lane group of the
+  // LDS store covers whole 32-B rows: conflict-free)
+  constexpr int KPT = TL::KPT, KG = 16 / KPT;
+  const int trow = tid / KG, tkg = tid % KG;
+  float2 ra[2][KPT], rb[2][KPT];
+  auto load = [&](auto set, int t) {
+    constexpr int S = decltype(set)::value;
+    const float2* pa = A + ((int64_t)t * BK + tkg * KPT) * g.lda + trow;
+    const float2* pb = B + ((int64_t)t * BK + tkg * KPT) * g.ldb + trow;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) ra[S][j] = pa[j * g.lda];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) rb[S][j] = pb[j * g.ldb];
+  };
+  // term planes: 0..2 = re (h, m, l), 3..5 = im (h, m, l)
+  const int toff = swz(trow, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
+  auto put = [&](const float2 (&v)[KPT], char* base, int sub) {
+    float re[KPT], im[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) { re[j] = v[j].x; im[j] = v[j].y; }
+    uint32_t h[KPT / 2], m[KPT / 2], l[KPT / 2];
+    splitn<KPT>(re, h, m, l);
+    st_lds<KPT>(base + 0 * sub + toff, h);
+    st_lds<KPT>(base + 1 * sub + toff, m);
+    st_lds<KPT>(base + 2 * sub + toff, l);
+    splitn<KPT>(im, h, m, l);
+    st_lds<KPT>(base + 3 * sub + toff, h);
+    st_lds<KPT>(base + 4 * sub + toff, m);
+    st_lds<KPT>(base + 5 * sub + toff, l);
+  };
+  auto store_stage = [&](auto set, int buf) {
+    constexpr int S = decltype(set)::value;
+    char* baseA = lds + buf * BUF;
+    put(ra[S], baseA, SUBA);
+    put(rb[S], baseA + 6 * SUBA, SUBB);
+  };
+
+  f32x16 acc[2][TI][TJ];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  int a_off[TI], b_off[TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) a_off[i] = swz(wm * TL::WM + i * 32 + fr, fh);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) b_off[j] = 6 * SUBA + swz(wn * TL::WN + j * 32 + fr, fh);
+
+  typedef uint4 FragA[6][TI];
+  typedef uint4 FragB[6][TJ];
+  auto read_frags = [&](const char* s, FragA& fa, FragB& fb) {
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) fa[x][i] = *reinterpret_cast<const uint4*>(s + x * SUBA + a_off[i]);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) fb[x][j] = *reinterpret_cast<const uint4*>(s + x * SUBB + b_off[j]);
+    }
+  };
+  // pairs of (A term, B term), smallest first
+  constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
+  constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
+  auto mfmas = [&](const FragA& fa, const FragB& fb) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const bf16x8 ar = __builtin_bit_cast(bf16x8, fa[PA[q]][i]);
+        const bf16x8 ai = __builtin_bit_cast(bf16x8, fa[3 + PA[q]][i]);
+        const bf16x8 nai = __builtin_bit_cast(bf16x8, neg8(fa[3 + PA[q]][i]));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const bf16x8 br = __builtin_bit_cast(bf16x8, fb[PB[q]][j]);
+          const bf16x8 bi = __builtin_bit_cast(bf16x8, fb[3 + PB[q]][j]);
+          acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar, br, acc[0][i][j], 0, 0, 0);
+          acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar, bi, acc[1][i][j], 0, 0, 0);
+          acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(nai, bi, acc[0][i][j], 0, 0, 0);
+          acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, br, acc[1][i][j], 0, 0, 0);
+        }
+      }
+  };
+  // one steady-state K-step t (t + 1 < nkt): fragments of step t, loads of step t + 2 into the
+  // register set step t used, split of step t + 1 (other set) into the other LDS half, MFMAs
+  auto body = [&](auto par, int t) {
+    constexpr int P = decltype(par)::value;
+    FragA fa;
+    FragB fb;
+    read_frags(lds + P * BUF, fa, fb);
+    load(std::integral_constant<int, P>{}, t + 2 < nkt ? t + 2 : nkt - 1);
+    store_stage(std::integral_constant<int, P ^ 1>{}, P ^ 1);
+    mfmas(fa, fb);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+
+  load(std::integral_constant<int, 0>{}, 0);
+  load(std::integral_constant<int, 1>{}, nkt > 1 ? 1 : 0);
+  store_stage(std::integral_constant<int, 0>{}, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  int t = 0;
+  for (; t + 2 < nkt; t += 2) {
+    body(std::integral_constant<int, 0>{}, t);
+    body(std::integral_constant<int, 1>{}, t + 1);
+  }
+  if (t + 1 < nkt) {
+    body(std::integral_constant<int, 0>{}, t);
+    ++t;
+  }
+  {
+    FragA fa;
+    FragB fb;
+    read_frags(lds + (t & 1) * BUF, fa, fb);
+    mfmas(fa, fb);
+  }
+
+  const bool partial = g.splits > 1;
+  float* Cout = partial ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * 2 : g.C + (int64_t)b * g.sC * 2;
+  const int64_t ldo = partial ? g.N : g.ldc;
+  const float beta = partial ? 0.f : g.beta;
+  auto store = [&](auto with_beta) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t gm = m0 + wm * TL::WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int64_t gn = n0 + wn * TL::WN + j * 32 + (lane & 31);
+          float2* p = reinterpret_cast<float2*>(Cout + (gm * ldo + gn) * 2);
+          float2 v = make_float2(acc[0][i][j][r], acc[1][i][j][r]);
+          if constexpr (decltype(with_beta)::value) {
+            const float2 o = *p;
+            v.x += beta * o.x;
+            v.y += beta * o.y;
+          }
+          *p = v;
+        }
+  };
+  if (beta != 0.f) store(std::true_type{});
+  else store(std::false_type{});
+}
+
+// ---------------------------------------------------------------------------------------------
 // FP64 fast path: float64 / complex128 with both operands K-outer (A stored K x M, B K x N) — the
 // same layout as the complex64 fast path, for the fp64 workloads (the symmetry-breaking ansatz,
 // BASELINE config 5) — on v_mfma_f64_16x16x4_f64.
@@ -801,6 +1069,7 @@ int fast_c64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, i
   return s;
 }
 int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (gemm_bf16()) return fast_c64_splits_t<xbf::TileX>(transA, transB, M, N, K, batch);
   if (!gemm_3m()) return fast_c64_splits_t<fastc64::Tile4M>(transA, transB, M, N, K, batch);
   return fast_c64_splits_t<fastc64::Tile3M>(transA, transB, M, N, K, batch);
 }
@@ -852,6 +1121,23 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       f.lda = lda; f.ldb = ldb; f.ldc = ldc; f.sA = sA; f.sB = sB; f.sC = sC; f.M = M; f.N = N;
       const bool g3 = gemm_3m();
       f.kchunk = K / fs;
+      f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;
+      if (gemm_bf16()) {
+        using TX = xbf::TileX;
+        f.mt = (int)(M / TX::BM);
+        f.nt = (int)(N / TX::BN);
+        const int64_t nb = (int64_t)f.mt * f.nt * fs * batch;
+        hipLaunchKernelGGL((gemm_c64_kouter_bf16_kernel<TX>), dim3((unsigned)nb), dim3(TX::NT), 0, stream, f);
+        TQ_HIP(hipGetLastError());
+        if (fs > 1) {
+          const int64_t total = batch * M * N * 2;
+          const int blocks = (int)std::min<int64_t>((total + kThreads - 1) / kThreads, 4096);
+          hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(blocks), dim3(kThreads), 0, stream,
+                             (const float*)W, (float*)C, M, N, ldc, sC, batch, fs, 2, (float)beta);
+          TQ_HIP(hipGetLastError());
+        }
+        return TQ_OK;
+      }
       f.mt = (int)(M / (g3 ? fastc64::Tile3M::BM : fastc64::Tile4M::BM));
       f.nt = (int)(N / (g3 ? fastc64::Tile3M::BN : fastc64::Tile4M::BN));
       f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;

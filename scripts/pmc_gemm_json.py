@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarize the PMC passes of scripts/pmc_gemm_bf16.sh into profiles/pmc_gemm_bf16_r02.json:
+MFMA busy fraction of the bf16-split boundary GEMM (SQ_VALU_MFMA_BUSY_CYCLES advances 32 cycles
+per v_mfma_f32_32x32x16_bf16), the effective shader clock (GRBM_GUI_ACTIVE summed over the 8
+XCDs / kernel duration), and HBM bytes per launch (FETCH_SIZE doubled per the gfx950 correction
+in MI355X_MICROARCH.md's HBM section, + WRITE_SIZE)."""
+import collections, csv, json, sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_gemm_bf16_r02.json"
+frag = "gemm_c64_kouter_bf16"
+
+
+def passes(d):
+    agg = collections.defaultdict(list)
+    n = set()
+    for r in csv.DictReader(open(f"{root}/{d}/run_counter_collection.csv")):
+        if frag not in r["Kernel_Name"]:
+            continue
+        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        n.add(r["Dispatch_Id"])
+    return {k: sum(v) / len(v) for k, v in agg.items()}, len(n)
+
+
+c1, n1 = passes("pmcx1")
+c2, _ = passes("pmcx2")
+c3, _ = passes("pmcx3")
+# kernel duration from the kernel-trace pass (same command, no counters)
+dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(f"{root}/ktx/run_kernel_trace.csv"))
+       if frag in r["Kernel_Name"]]
+avg_ns = sum(dur) / len(dur)
+M = N = 1024
+K = 65536
+n_mfma = 24 * (M // 32) * (N // 32) * (K // 16)      # 4M x 6 split products per 32x32x16 tile-step
+cyc_xcd = c1["GRBM_GUI_ACTIVE"] / 8
+res = {
+    "config": "C4",
+    "kernel": "gemm_c64_kouter_bf16_kernel<Tile<2,4,2,1>> (complex64 via exact 3-term bf16 split, 4M, "
+              "M=N=1024, K=65536 per slice, block 128x128, split-K 4)",
+    "command": "scripts/pmc_gemm_bf16.sh (rocprofv3 --pmc ... --kernel-include-regex gemm_c64 -- python3 bench.py "
+               "--no-cpu-baseline --no-c5 --steps 2 --warmup 1; FETCH_SIZE and WRITE_SIZE in separate passes; "
+               "durations from a --kernel-trace pass)",
+    "launches": n1,
+    "counters_avg_per_launch": c1,
+    "expected_mfma_per_launch": n_mfma,
+    "busy_cycles_per_mfma": c1["SQ_VALU_MFMA_BUSY_CYCLES"] / n_mfma,
+    "avg_launch_ns_trace": avg_ns,
+    "cycles_per_xcd": cyc_xcd,
+    "effective_clock_GHz": cyc_xcd / avg_ns,
+    "mfma_busy_frac": c1["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc_xcd * 256 * 4),
+    "FETCH_SIZE_kB_per_launch": c2.get("FETCH_SIZE"),
+    "WRITE_SIZE_kB_per_launch": c3.get("WRITE_SIZE"),
+    "hbm_bytes_per_launch": (2 * c2.get("FETCH_SIZE", 0) + c3.get("WRITE_SIZE", 0)) * 1024,
+    "algorithmic_bytes_per_launch": (M * K + N * K) * 8 + 4 * M * N * 8,
+    "definition": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 XCDs * 256 CUs * 4 SIMDs); "
+                  "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (kB, gfx950 FETCH correction); algorithmic bytes = "
+                  "A + B once + the 4 split-K partial slabs written",
+}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
