@@ -18,6 +18,7 @@ const std::string& last_error() { return g_last_error; }
 namespace tq {
 bool gemm_3m();
 bool gemm_bf16();
+bool gemm_f16();
 bool gemm_configure(const char* key, int64_t v);
 bool graphs_enabled();
 bool sweeps_enabled_global();
@@ -28,6 +29,7 @@ extern "C" int64_t tq_library_query(const char* key) {
   const std::string k(key);
   if (k == "gemm_3m") return tq::gemm_3m() ? 1 : 0;
   if (k == "gemm_bf16") return tq::gemm_bf16() ? 1 : 0;
+  if (k == "gemm_f16") return tq::gemm_f16() ? 1 : 0;
   if (k == "graphs") return tq::graphs_enabled() ? 1 : 0;
   if (k == "sweep") return tq::sweeps_enabled_global() ? 1 : 0;
 

@@ -33,17 +33,23 @@ static int env_flag(const char* name) {
 }
 static std::atomic<int> g_gemm_3m{env_flag("TQ_GEMM_3M")};
 static std::atomic<int> g_gemm_bf16{env_flag("TQ_GEMM_BF16")};
+static std::atomic<int> g_gemm_f16{env_flag("TQ_GEMM_F16")};
 bool gemm_3m() { return g_gemm_3m.load(std::memory_order_relaxed) != 0; }
 // The complex64 K-outer fast path runs on the bf16 matrix cores with an exact 3-term split of
-// every f32 operand (gemm_c64_kouter_bf16_kernel, f32 accuracy); TQ_GEMM_BF16=0 (or
+// every f32 operand (gemm_c64_kouter_split_kernel<TileX, SplitBF16>, f32 accuracy); TQ_GEMM_BF16=0 (or
 // tq_library_set("gemm_bf16", 0)) selects the f32-MFMA kernel.
 bool gemm_bf16() { return g_gemm_bf16.load(std::memory_order_relaxed) != 0; }
+// ... and, by default, on the f16 matrix cores with a 2-term split of the power-of-two-scaled
+// operands (gemm_c64_kouter_split_kernel<TileH, SplitF16>, f32 accuracy, half the MFMAs of the
+// bf16 3-term split); TQ_GEMM_F16=0 (or tq_library_set("gemm_f16", 0)) keeps the bf16 split.
+bool gemm_f16() { return g_gemm_f16.load(std::memory_order_relaxed) != 0; }
 // runtime switch (tq_library_set): affects launches issued after the call (plans replaying a
 // captured hipGraph keep the kernels they captured)
 bool gemm_configure(const char* key, int64_t v) {
   const std::string k(key);
   if (k == "gemm_3m") { g_gemm_3m = v ? 1 : 0; return true; }
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
+  if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
   return false;
 }
 
@@ -94,6 +100,7 @@ struct GemmArgs {
 };
 
 constexpr int kThreads = 256;
+constexpr size_t kAmaxBytes = 256;  // f16 split: max-word block behind the split-K slabs
 
 // TQ_GEMM_FAST=0 disables the K-outer complex64 fast path (A/B timing of the two kernels)
 bool fast_disabled() {
@@ -381,6 +388,7 @@ struct FastArgs {
   int64_t kchunk;  // K per split (multiple of BK)
   int mt, nt, splits, batch;
   float beta;
+  const uint32_t* amax;  // f16 split kernel: max |x| bits of A and B (absmax_kouter_kernel)
 };
 
 template <int N>
@@ -592,43 +600,100 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
 // 16 distinct bank slots (PMC SQ_LDS_BANK_CONFLICT = 0).  One barrier per K-step.
 namespace xbf {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-template <int WMW_, int WNW_, int TI_, int TJ_> struct Tile {
-  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_> struct Tile {
+  static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_, NTERM = NTERM_;
   static constexpr int NW = WMW * WNW, NT = 64 * NW;
   static constexpr int WM = 32 * TI, WN = 32 * TJ, BM = WMW * WM, BN = WNW * WN, BK = 16;
   static constexpr int SUBA = BM * 32, SUBB = BN * 32;            // bytes per term plane
-  static constexpr int BUF = 6 * (SUBA + SUBB);                   // 2 planes x 3 terms, A and B
+  static constexpr int BUF = 2 * NTERM * (SUBA + SUBB);           // 2 planes x NTERM terms, A and B
   // one split task per thread and operand: KPT consecutive k of one row
   static constexpr int KPT = 16 * BM / NT;
   static_assert(BM == BN && (KPT == 4 || KPT == 8), "task split");
   static_assert(2 * BUF <= 160 * 1024, "LDS");
 };
-// 8 waves (two per SIMD) of 64 x 32, block 128 x 128: 2 x 48 KiB LDS, 64 accumulators per wave;
-// 4-k split tasks (ds_write_b64)
-using TileX = Tile<2, 4, 2, 1>;
+// 8 waves (two per SIMD) of 64 x 32, block 128 x 128, 64 accumulators per wave; 4-k split tasks
+// (ds_write_b64).  bf16: 3 terms, 2 x 48 KiB LDS; f16: 2 terms, 2 x 32 KiB.
+using TileX = Tile<2, 4, 2, 1, 3>;
+using TileH = Tile<2, 4, 2, 1, 2>;
 
 __device__ __forceinline__ uint32_t hi16(float x) { return __float_as_uint(x) & 0xffff0000u; }
 // pack the bf16 held in the high halves of two dwords: lo <- a, hi <- b
 __device__ __forceinline__ uint32_t pk(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
 
-// split N values into three packed bf16 terms (h, m, l; N/2 dwords each), exactly
-template <int N>
-__device__ __forceinline__ void splitn(const float (&v)[N], uint32_t (&h)[N / 2], uint32_t (&m)[N / 2], uint32_t (&l)[N / 2]) {
-  uint32_t hb[N], mb[N], lb[N];
+// bf16, three terms by truncation: h = x with the low 16 bits cleared, r = x - h (exact),
+// m = r truncated the same way, l = r - m (exact, <= 8 significant bits): x == h + m + l exactly.
+// Term pairs kept (A term, B term), smallest first: mh hm lh hl hh... the six down to 2^-16.
+struct SplitBF16 {
+  static constexpr int NTERM = 3, NPAIR = 6;
+  static constexpr bool SCALED = false;
+  static constexpr int NSET = 2;  // staging register sets (4 spill at 3 terms)
+  static constexpr int pa(int q) { return q == 0 ? 1 : q == 2 ? 2 : q == 4 ? 1 : 0; }  // 1 0 2 0 1 0
+  static constexpr int pb(int q) { return q == 0 ? 1 : q == 1 ? 2 : q == 3 ? 1 : 0; }  // 1 2 0 1 0 0
+  template <int N>
+  static __device__ __forceinline__ void split(const float (&v)[N], int, uint32_t (&t)[3][N / 2]) {
+    uint32_t hb[N], mb[N], lb[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    hb[j] = hi16(v[j]);
-    const float r = v[j] - __uint_as_float(hb[j]);
-    mb[j] = hi16(r);
-    lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
-  }
+    for (int j = 0; j < N; ++j) {
+      hb[j] = hi16(v[j]);
+      const float r = v[j] - __uint_as_float(hb[j]);
+      mb[j] = hi16(r);
+      lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
+    }
 #pragma unroll
-  for (int j = 0; j < N / 2; ++j) {
-    h[j] = pk(hb[2 * j], hb[2 * j + 1]);
-    m[j] = pk(mb[2 * j], mb[2 * j + 1]);
-    l[j] = pk(lb[2 * j], lb[2 * j + 1]);
+    for (int j = 0; j < N / 2; ++j) {
+      t[0][j] = pk(hb[2 * j], hb[2 * j + 1]);
+      t[1][j] = pk(mb[2 * j], mb[2 * j + 1]);
+      t[2][j] = pk(lb[2 * j], lb[2 * j + 1]);
+    }
   }
+  static __device__ __forceinline__ f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+
+// f16, two terms of a power-of-two-scaled value: xs = x * 2^sc (sc from the operand's max |x|,
+// so max |xs| is in [2^14, 2^15)), h = f16(xs) (round to nearest), r = xs - h (exact in f32,
+// |r| <= 2^-12 |xs|), l = f16(r): xs == h + l within 2^-24 |xs| (l's rounding) — the f32 rounding
+// level — for |xs| >= 2^-2 (l normal); below that l's absolute error is <= 2^-25, i.e. <= 2^-40 of
+// the operand's max.  Pairs kept: lh, hl, hh; the dropped ll is <= 2^-24 relative.
+struct SplitF16 {
+  static constexpr int NTERM = 2, NPAIR = 3;
+  static constexpr bool SCALED = true;
+  static constexpr int NSET = 4;
+  static constexpr int pa(int q) { return q == 0 ? 1 : 0; }  // 1 0 0
+  static constexpr int pb(int q) { return q == 1 ? 1 : 0; }  // 0 1 0
+  // per pair of values: 2 v_ldexp_f32, v_cvt_pk_f16_f32 (h), 2 v_fma_mix_f32 (r = x - h, reading
+  // the packed f16 halves directly), v_cvt_pk_f16_f32 (l): 3 VALU per value
+  template <int N>
+  static __device__ __forceinline__ void split(const float (&v)[N], int sc, uint32_t (&t)[2][N / 2]) {
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) {
+      const float x0 = ldexpf(v[2 * j], sc), x1 = ldexpf(v[2 * j + 1], sc);
+      const f16x2 hv = {(_Float16)x0, (_Float16)x1};
+      const uint32_t h = __builtin_bit_cast(uint32_t, hv);
+      float r0, r1;
+      asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r0) : "v"(x0), "v"(h));
+      asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r1) : "v"(x1), "v"(h));
+      const f16x2 lv = {(_Float16)r0, (_Float16)r1};
+      t[0][j] = h;
+      t[1][j] = __builtin_bit_cast(uint32_t, lv);
+    }
+  }
+  static __device__ __forceinline__ f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+// exponent sc with max|x| * 2^sc in [2^14, 2^15) from the bits of max|x| (0 -> 0; inf/nan -> 0)
+__device__ __forceinline__ int scale_exp(uint32_t bits) {
+  const int E = (int)((bits >> 23) & 0xff);
+  if (bits == 0 || E == 255) return 0;
+  const int e = E ? E - 127 : (31 - __clz((int)(bits & 0x7fffff))) - 149;
+  return 14 - e;
 }
+
 template <int N>
 __device__ __forceinline__ void st_lds(char* p, const uint32_t (&w)[N / 2]) {
   if constexpr (N == 8) *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -637,16 +702,54 @@ __device__ __forceinline__ void st_lds(char* p, const uint32_t (&w)[N / 2]) {
 
 // byte offset of (row, k-half) inside a term plane
 __device__ __forceinline__ int swz(int row, int kh) { return row * 32 + ((kh ^ ((row >> 3) & 1)) << 4); }
+// sign flip of 8 packed 16-bit floats (bf16 and f16 keep the sign in bit 15)
 __device__ __forceinline__ uint4 neg8(uint4 v) {
   return make_uint4(v.x ^ 0x80008000u, v.y ^ 0x80008000u, v.z ^ 0x80008000u, v.w ^ 0x80008000u);
 }
+
+// max |re|, |im| over the K x M (A) and K x N (B) operands of every batch, as float bits
+// atomically max-ed into amax[0] (A) / amax[1] (B) (zeroed before).  One wave per k-row,
+// 64 lanes x 16 B per load, four loads in flight; rows are M / 2 float4 (M % 128 == 0).
+__global__ void __launch_bounds__(256) absmax_kouter_kernel(const float4* A, int64_t lda4, int64_t sA4,
+                                                            const float4* B, int64_t ldb4, int64_t sB4,
+                                                            int64_t K, int64_t w4A, int64_t w4B,
+                                                            int64_t batch, uint32_t* amax) {
+  const int op = blockIdx.y;
+  const float4* base = op ? B : A;
+  const int64_t ld = op ? ldb4 : lda4, s = op ? sB4 : sA4, w = op ? w4B : w4A;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4, rows = K * batch;
+  float m = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const int64_t b = r / K, k = r - b * K;
+    const float4* p = base + b * s + k * ld + lane;
+    for (int64_t c = 0; c < w; c += 256) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (c + 64 * u < w) ? p[c + 64 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float red[4];
+  if (lane == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(amax + op, __float_as_uint(m));
+  }
+}
 }  // namespace xbf
 
-template <typename TL>
-__global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArgs g) {
+template <typename TL, typename SP>
+__global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastArgs g) {
   using namespace xbf;
   constexpr int BM = TL::BM, BN = TL::BN, BK = TL::BK, WMW = TL::WMW, TI = TL::TI, TJ = TL::TJ;
-  constexpr int SUBA = TL::SUBA, SUBB = TL::SUBB, BUF = TL::BUF;
+  constexpr int SUBA = TL::SUBA, SUBB = TL::SUBB, BUF = TL::BUF, NTM = SP::NTERM;
+  static_assert(TL::NTERM == SP::NTERM, "tile / split terms");
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -669,43 +772,65 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArg
 
   const float2* A = reinterpret_cast<const float2*>(g.A) + ((int64_t)b * g.sA + kbeg * g.lda + m0);
   const float2* B = reinterpret_cast<const float2*>(g.B) + ((int64_t)b * g.sB + kbeg * g.ldb + n0);
+  // power-of-two operand scales (f16 terms): from the operands' max |x| (absmax_kouter_kernel)
+  int sca = 0, scb = 0;
+  if constexpr (SP::SCALED) {
+    sca = scale_exp(g.amax[0]);
+    scb = scale_exp(g.amax[1]);
+  }
 
-  // staging registers, two sets (K-step parity): KPT complex (k0 .. k0+KPT-1 of one row);
-  // task = thread: row = tid / (16 / KPT), k-group = tid % (16 / KPT) (a 16-lane group of the
-  // LDS store covers whole 32-B rows: conflict-free)
-  constexpr int KPT = TL::KPT, KG = 16 / KPT;
-  const int trow = tid / KG, tkg = tid % KG;
-  float2 ra[2][KPT], rb[2][KPT];
+  // staging registers, NSET sets (K-step mod NSET).  Threads 0 .. NT/2-1 stage A, the rest B
+  // (wave-uniform); a thread owns rows 2r, 2r+1 (r = lane-group index) x KPT = 4 consecutive k
+  // (k-group tkg = tid % 4): per K-step four 16-B loads (one k, both rows: a wave-instruction
+  // covers 4 k-rows x 256 B) and, per row and term plane, one 8-B LDS store (a 16-lane group
+  // writes rows 0, 2, 4, 6 (+8..) x 32 B: distinct banks).  Per-CU L2 -> L1 request concurrency,
+  // not bandwidth, bounded the 8-B-per-lane version (512 B per wave-load): ~7.5 B/clk/CU with the
+  // MFMAs removed.  A K-step's loads are issued NSET - 1 K-steps before its split.
+  constexpr int KPT = 4, NSET = SP::NSET;
+  static_assert(TL::NT == 4 * BM && BM == BN, "two operands x BM/2 row pairs x 4 k-groups");
+  const int op = __builtin_amdgcn_readfirstlane(tid >= TL::NT / 2 ? 1 : 0);  // wave-uniform: SGPR
+  const int ot = tid & (TL::NT / 2 - 1);
+  const int trow = 2 * (ot >> 2), tkg = ot & 3;
+  float4 rv[NSET][KPT];
+  // wave-uniform K-step base (SGPR pair) + per-lane 32-bit byte offsets fixed over the loop (no
+  // per-step address VALU; launch: lda, ldb < 2^24 complex)
+  const int64_t ld = op ? g.ldb : g.lda;
+  const char* src = reinterpret_cast<const char*>(op ? B : A);
+  uint32_t off[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) off[j] = (uint32_t)(((tkg * KPT + j) * ld + trow) * 8);
+  const int64_t stepb = (int64_t)BK * ld * 8;
   auto load = [&](auto set, int t) {
     constexpr int S = decltype(set)::value;
-    const float2* pa = A + ((int64_t)t * BK + tkg * KPT) * g.lda + trow;
-    const float2* pb = B + ((int64_t)t * BK + tkg * KPT) * g.ldb + trow;
+    const char* p = src + t * stepb;
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) ra[S][j] = pa[j * g.lda];
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) rb[S][j] = pb[j * g.ldb];
+    for (int j = 0; j < KPT; ++j) rv[S][j] = *reinterpret_cast<const float4*>(p + off[j]);
   };
-  // term planes: 0..2 = re (h, m, l), 3..5 = im (h, m, l)
-  const int toff = swz(trow, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
-  auto put = [&](const float2 (&v)[KPT], char* base, int sub) {
-    float re[KPT], im[KPT];
+  // term planes: 0..NTM-1 = re terms (largest first), NTM..2 NTM-1 = im terms
+  const int sc = op ? scb : sca;
+  const int sub = op ? SUBB : SUBA;
+  const int obase = op ? 2 * NTM * SUBA : 0;
+  const int toff0 = swz(trow, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
+  const int toff1 = swz(trow + 1, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
+  auto put = [&](const float (&re)[KPT], const float (&im)[KPT], char* base, int toff) {
+    uint32_t t[NTM][KPT / 2];
+    SP::template split<KPT>(re, sc, t);
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) { re[j] = v[j].x; im[j] = v[j].y; }
-    uint32_t h[KPT / 2], m[KPT / 2], l[KPT / 2];
-    splitn<KPT>(re, h, m, l);
-    st_lds<KPT>(base + 0 * sub + toff, h);
-    st_lds<KPT>(base + 1 * sub + toff, m);
-    st_lds<KPT>(base + 2 * sub + toff, l);
-    splitn<KPT>(im, h, m, l);
-    st_lds<KPT>(base + 3 * sub + toff, h);
-    st_lds<KPT>(base + 4 * sub + toff, m);
-    st_lds<KPT>(base + 5 * sub + toff, l);
+    for (int x = 0; x < NTM; ++x) st_lds<KPT>(base + x * sub + toff, t[x]);
+    SP::template split<KPT>(im, sc, t);
+#pragma unroll
+    for (int x = 0; x < NTM; ++x) st_lds<KPT>(base + (NTM + x) * sub + toff, t[x]);
   };
   auto store_stage = [&](auto set, int buf) {
     constexpr int S = decltype(set)::value;
-    char* baseA = lds + buf * BUF;
-    put(ra[S], baseA, SUBA);
-    put(rb[S], baseA + 6 * SUBA, SUBB);
+    char* base = lds + buf * BUF + obase;
+    float r0[KPT], i0[KPT], r1[KPT], i1[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      r0[j] = rv[S][j].x; i0[j] = rv[S][j].y; r1[j] = rv[S][j].z; i1[j] = rv[S][j].w;
+    }
+    put(r0, i0, base, toff0);
+    put(r1, i1, base, toff1);
   };
 
   f32x16 acc[2][TI][TJ];
@@ -723,13 +848,13 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArg
 #pragma unroll
   for (int i = 0; i < TI; ++i) a_off[i] = swz(wm * TL::WM + i * 32 + fr, fh);
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) b_off[j] = 6 * SUBA + swz(wn * TL::WN + j * 32 + fr, fh);
+  for (int j = 0; j < TJ; ++j) b_off[j] = 2 * NTM * SUBA + swz(wn * TL::WN + j * 32 + fr, fh);
 
-  typedef uint4 FragA[6][TI];
-  typedef uint4 FragB[6][TJ];
+  typedef uint4 FragA[2 * NTM][TI];
+  typedef uint4 FragB[2 * NTM][TJ];
   auto read_frags = [&](const char* s, FragA& fa, FragB& fb) {
 #pragma unroll
-    for (int x = 0; x < 6; ++x) {
+    for (int x = 0; x < 2 * NTM; ++x) {
 #pragma unroll
       for (int i = 0; i < TI; ++i) fa[x][i] = *reinterpret_cast<const uint4*>(s + x * SUBA + a_off[i]);
 #pragma unroll
@@ -737,53 +862,65 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArg
     }
   };
   // pairs of (A term, B term), smallest first
-  constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
-  constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
   auto mfmas = [&](const FragA& fa, const FragB& fb) {
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
+    for (int q = 0; q < SP::NPAIR; ++q)
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const bf16x8 ar = __builtin_bit_cast(bf16x8, fa[PA[q]][i]);
-        const bf16x8 ai = __builtin_bit_cast(bf16x8, fa[3 + PA[q]][i]);
-        const bf16x8 nai = __builtin_bit_cast(bf16x8, neg8(fa[3 + PA[q]][i]));
+        const uint4 ar = fa[SP::pa(q)][i];
+        const uint4 ai = fa[NTM + SP::pa(q)][i];
+        const uint4 nai = neg8(ai);
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          const bf16x8 br = __builtin_bit_cast(bf16x8, fb[PB[q]][j]);
-          const bf16x8 bi = __builtin_bit_cast(bf16x8, fb[3 + PB[q]][j]);
-          acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar, br, acc[0][i][j], 0, 0, 0);
-          acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar, bi, acc[1][i][j], 0, 0, 0);
-          acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(nai, bi, acc[0][i][j], 0, 0, 0);
-          acc[1][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, br, acc[1][i][j], 0, 0, 0);
+          const uint4 br = fb[SP::pb(q)][j];
+          const uint4 bi = fb[NTM + SP::pb(q)][j];
+          acc[0][i][j] = SP::mfma(ar, br, acc[0][i][j]);
+          acc[1][i][j] = SP::mfma(ar, bi, acc[1][i][j]);
+          acc[0][i][j] = SP::mfma(nai, bi, acc[0][i][j]);
+          acc[1][i][j] = SP::mfma(ai, br, acc[1][i][j]);
         }
       }
   };
-  // one steady-state K-step t (t + 1 < nkt): fragments of step t, loads of step t + 2 into the
-  // register set step t used, split of step t + 1 (other set) into the other LDS half, MFMAs
+  // one steady-state K-step t (t + 1 < nkt, P = t mod NSET): loads of step t + NSET into the
+  // register set step t used (split one step ago) issued first, then the fragments of step t,
+  // the split of step t + 1 into the other LDS half, the MFMAs
   auto body = [&](auto par, int t) {
     constexpr int P = decltype(par)::value;
+    load(std::integral_constant<int, P>{}, t + NSET < nkt ? t + NSET : nkt - 1);
+    __builtin_amdgcn_sched_barrier(0);
     FragA fa;
     FragB fb;
-    read_frags(lds + P * BUF, fa, fb);
-    load(std::integral_constant<int, P>{}, t + 2 < nkt ? t + 2 : nkt - 1);
-    store_stage(std::integral_constant<int, P ^ 1>{}, P ^ 1);
+    read_frags(lds + (P & 1) * BUF, fa, fb);
+    store_stage(std::integral_constant<int, (P + 1) % NSET>{}, (P & 1) ^ 1);
     mfmas(fa, fb);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
 
+  static_assert(NSET == 2 || NSET == 4, "unrolled by NSET below");
   load(std::integral_constant<int, 0>{}, 0);
-  load(std::integral_constant<int, 1>{}, nkt > 1 ? 1 : 0);
+  load(std::integral_constant<int, 1>{}, nkt > 1 ? 1 : nkt - 1);
+  if constexpr (NSET == 4) {
+    load(std::integral_constant<int, NSET == 4 ? 2 : 0>{}, nkt > 2 ? 2 : nkt - 1);
+    load(std::integral_constant<int, NSET == 4 ? 3 : 0>{}, nkt > 3 ? 3 : nkt - 1);
+  }
   store_stage(std::integral_constant<int, 0>{}, 0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   int t = 0;
-  for (; t + 2 < nkt; t += 2) {
+  for (; t + NSET < nkt; t += NSET) {
     body(std::integral_constant<int, 0>{}, t);
     body(std::integral_constant<int, 1>{}, t + 1);
+    if constexpr (NSET == 4) {
+      body(std::integral_constant<int, NSET == 4 ? 2 : 0>{}, t + 2);
+      body(std::integral_constant<int, NSET == 4 ? 3 : 0>{}, t + 3);
+    }
   }
-  if (t + 1 < nkt) {
-    body(std::integral_constant<int, 0>{}, t);
-    ++t;
+  // 1 .. NSET steps left: all but the last split their successor
+  if (t + 1 < nkt) body(std::integral_constant<int, 0>{}, t);
+  if constexpr (NSET == 4) {
+    if (t + 2 < nkt) body(std::integral_constant<int, 1>{}, t + 1);
+    if (t + 3 < nkt) body(std::integral_constant<int, NSET == 4 ? 2 : 0>{}, t + 2);
   }
+  t = nkt - 1;
   {
     FragA fa;
     FragB fb;
@@ -795,6 +932,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArg
   float* Cout = partial ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * 2 : g.C + (int64_t)b * g.sC * 2;
   const int64_t ldo = partial ? g.N : g.ldc;
   const float beta = partial ? 0.f : g.beta;
+  const int unsc = -(sca + scb);
   auto store = [&](auto with_beta) {
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -805,7 +943,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_bf16_kernel(FastArg
           const int64_t gm = m0 + wm * TL::WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int64_t gn = n0 + wn * TL::WN + j * 32 + (lane & 31);
           float2* p = reinterpret_cast<float2*>(Cout + (gm * ldo + gn) * 2);
-          float2 v = make_float2(acc[0][i][j][r], acc[1][i][j][r]);
+          float2 v = make_float2(ldexpf(acc[0][i][j][r], unsc), ldexpf(acc[1][i][j][r], unsc));
           if constexpr (decltype(with_beta)::value) {
             const float2 o = *p;
             v.x += beta * o.x;
@@ -1113,7 +1251,8 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
   if constexpr (CPLX && sizeof(R) == 4) {
     const int fs = fast_c64_splits(transA, transB, M, N, K, batch);
     const bool al = ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && lda % 2 == 0 &&
-                    ldb % 2 == 0 && (batch == 1 || (sA % 2 == 0 && sB % 2 == 0));
+                    ldb % 2 == 0 && (batch == 1 || (sA % 2 == 0 && sB % 2 == 0)) &&
+                    lda < (int64_t(1) << 24) && ldb < (int64_t(1) << 24);
     const size_t need = (size_t)fs * batch * M * N * 8;
     if (fs > 0 && al && (fs == 1 || (W != nullptr && wsb >= need)) && !fast_disabled()) {
       FastArgs f{};
@@ -1124,10 +1263,28 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;
       if (gemm_bf16()) {
         using TX = xbf::TileX;
+        static_assert(TX::BM == xbf::TileH::BM && TX::BN == xbf::TileH::BN, "same split-K tiling");
         f.mt = (int)(M / TX::BM);
         f.nt = (int)(N / TX::BN);
         const int64_t nb = (int64_t)f.mt * f.nt * fs * batch;
-        hipLaunchKernelGGL((gemm_c64_kouter_bf16_kernel<TX>), dim3((unsigned)nb), dim3(TX::NT), 0, stream, f);
+        // the f16 split needs the two max words behind the split-K slabs
+        const size_t slab = fs > 1 ? need : 0;
+        if (gemm_f16() && W != nullptr && wsb >= slab + kAmaxBytes) {
+          uint32_t* amax = reinterpret_cast<uint32_t*>(static_cast<char*>(W) + slab);
+          TQ_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), stream));
+          const int64_t rows = K * batch;
+          const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1024));
+          hipLaunchKernelGGL(xbf::absmax_kouter_kernel, dim3(gx, 2), dim3(256), 0, stream,
+                             (const float4*)A, lda / 2, sA / 2, (const float4*)B, ldb / 2, sB / 2, K,
+                             M / 2, N / 2, batch, amax);
+          TQ_HIP(hipGetLastError());
+          f.amax = amax;
+          hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitF16>), dim3((unsigned)nb),
+                             dim3(xbf::TileH::NT), 0, stream, f);
+        } else {
+          hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<TX, xbf::SplitBF16>), dim3((unsigned)nb),
+                             dim3(TX::NT), 0, stream, f);
+        }
         TQ_HIP(hipGetLastError());
         if (fs > 1) {
           const int64_t total = batch * M * N * 2;
@@ -1265,10 +1422,12 @@ size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch)
   }
   const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   int s = choose_splits(tiles, K, (int)bk);
-  if (dtype == TQ_C64) s = std::max(s, fast_c64_splits(1, 0, M, N, K, batch));
+  // the complex64 fast path also keeps the f16 split's two operand max words (kAmaxBytes)
+  const int fs = dtype == TQ_C64 ? fast_c64_splits(1, 0, M, N, K, batch) : 0;
+  s = std::max(s, fs);
   if (dtype == TQ_F64 || dtype == TQ_C128) s = std::max(s, fast_f64_splits(dtype, 1, 0, M, N, K, batch));
-  if (s <= 1) return 0;
-  return (size_t)s * batch * M * N * dtype_size(dtype);
+  const size_t slabs = s <= 1 ? 0 : (size_t)s * batch * M * N * dtype_size(dtype);
+  return fs > 0 ? slabs + kAmaxBytes : slabs;
 }
 
 int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,

@@ -133,16 +133,19 @@ def test_contract_pair_gate_apply(T, dev):
     assert np.abs(c - ref).max() / np.abs(ref).max() < 1e-5
 
 
-@pytest.fixture(params=["bf16", "f32"])
+@pytest.fixture(params=["f16", "bf16", "f32"])
 def c64_kernel(request):
-    """Runs a test once on each complex64 K-outer kernel: the bf16 3-term split kernel (default)
-    and the f32-MFMA LDS-DMA kernel (tq_library_set("gemm_bf16", 0)); restores the default."""
+    """Runs a test once on each complex64 K-outer kernel: the f16 2-term split of the scaled
+    operands (default), the bf16 3-term split kernel (tq_library_set("gemm_f16", 0)) and the
+    f32-MFMA LDS-DMA kernel (tq_library_set("gemm_bf16", 0)); restores the defaults."""
     import tneq_qc_amd._lib as _lib
     L = _lib.lib()
-    before = L.tq_library_query(b"gemm_bf16")
-    assert L.tq_library_set(b"gemm_bf16", 1 if request.param == "bf16" else 0) == 0
+    before = (L.tq_library_query(b"gemm_bf16"), L.tq_library_query(b"gemm_f16"))
+    assert L.tq_library_set(b"gemm_bf16", 0 if request.param == "f32" else 1) == 0
+    assert L.tq_library_set(b"gemm_f16", 1 if request.param == "f16" else 0) == 0
     yield request.param
-    L.tq_library_set(b"gemm_bf16", before)
+    L.tq_library_set(b"gemm_bf16", before[0])
+    L.tq_library_set(b"gemm_f16", before[1])
 
 
 @pytest.mark.parametrize("M,N,K,B,beta", [(256, 128, 16, 1, 0.0), (256, 128, 48, 3, 0.0),
@@ -164,6 +167,37 @@ def test_gemm_c64_kouter_fast_path(T, dev, c64_kernel, M, N, K, B, beta):
     ref = np.matmul(np.swapaxes(a.astype("complex128"), 1, 2), b.astype("complex128")) + beta * c0
     err = np.abs(cd.cpu().numpy() - ref).max() / np.abs(ref).max()
     assert err < TOL["complex64"], (M, N, K, B, err)
+
+
+@pytest.mark.parametrize("sa,sb", [(1e-30, 1e25), (1e20, 1e-12), (2e-32, 1e-3), (1.0, 0.0), (7.0, 1e-3)])
+def test_gemm_c64_split_operand_scales(T, dev, c64_kernel, sa, sb):
+    """Operand magnitudes far from 1 (the f16 split scales each operand by a power of two from its
+    max |x| into [2^14, 2^15)): tiny / huge / near-denormal / all-zero operands, a row block 2^-20
+    below the rest and a zero row, on every complex64 K-outer kernel, against complex128 —
+    2e-5 of max|C| (or exactly zero)."""
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(5)
+    M, N, K = 256, 128, 512
+    a = (_rand(rng, (1, K, M), "complex128") * sa)
+    b = (_rand(rng, (1, K, N), "complex128") * sb)
+    a[:, :, :64] *= 2.0 ** -20
+    b[:, 7, :] = 0
+    a, b = a.astype("complex64"), b.astype("complex64")
+    cd = _to(T, dev, np.zeros((1, M, N), "complex64"))
+    ops.gemm(_to(T, dev, a), _to(T, dev, b), True, False, out=cd)
+    ref = np.matmul(np.swapaxes(a.astype("complex128"), 1, 2), b.astype("complex128"))
+    got = cd.cpu().numpy()
+    assert np.isfinite(got).all()
+    if sb == 0.0:
+        assert np.all(got == 0)
+        return
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err < TOL["complex64"], (sa, sb, err)
+    # the 2^-20 row block keeps its own relative accuracy (no flush of the small values) where
+    # its products are f32-normal
+    if np.abs(ref[:, :64]).max() > 1e-30:
+        blk = np.abs(got[:, :64] - ref[:, :64]).max() / np.abs(ref[:, :64]).max()
+        assert blk < 1e-4, (sa, sb, blk)
 
 
 @pytest.mark.parametrize("dt", ["float64", "complex128"])
