@@ -35,7 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, f32-in MFMA
-PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA peak (no sparsity) at 2.4 GHz
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 / F16 dense MFMA peak (no sparsity) at 2.4 GHz
 PEAK_CLOCK_GHZ = 2.4
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 N_OPEN_CPU = 20                 # open outputs in the CPU-baseline sample (one slice: ~5-15 s of numpy)
@@ -180,18 +180,18 @@ def c5_train(dev, with_cpu: bool = True, steps: int = 5, warmup: int = 2):
     return r
 
 
-def alt_f32(args):
-    """The same headline with the boundary GEMM on the f32 MFMA kernel (TQ_GEMM_BF16=0, the
-    library reads it once per process: a child process, started without exec)."""
+def alt_gemm(args, var: str, desc: str):
+    """The same headline with another complex64 boundary-GEMM kernel (env `var`=0, read by the
+    library once per process: a child process, started without exec)."""
     import subprocess
-    env = dict(os.environ, TQ_GEMM_BF16="0")
+    env = dict(os.environ, **{var: "0"})
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", args.config, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
     return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
-            "gemm": "v_mfma_f32_32x32x2_f32 (TQ_GEMM_BF16=0)", "roofline": d["roofline"]}
+            "gemm": f"{desc} ({var}=0)", "roofline": d["roofline"]}
 
 
 def main():
@@ -278,17 +278,25 @@ def main():
     L = _lib.lib()
     g3m = bool(L.tq_library_query(b"gemm_3m") == 1)
     bf16 = bool(L.tq_library_query(b"gemm_bf16") == 1)
+    f16 = bf16 and bool(L.tq_library_query(b"gemm_f16") == 1)
     value = n_amp * args.steps / dt
     nl = max(1, gemm["launches"])
     avg_gemm_s = gemm["ms"] / 1e3 / nl
     alg_flops = gemm["flops"] / nl                      # 8*M*N*K complex GEMM flops per launch
-    # MFMA work executed per launch: bf16 split = 4 real products x 6 term products = 48*M*N*K;
-    # f32 3M = 6*M*N*K, f32 4M = 8*M*N*K
-    exe_flops = alg_flops * (6.0 if bf16 else (0.75 if g3m else 1.0))
+    # MFMA work executed per launch: f16 split = 4 real products x 3 term products = 24*M*N*K;
+    # bf16 split = 4 x 6 = 48*M*N*K; f32 3M = 6*M*N*K, f32 4M = 8*M*N*K
+    exe_flops = alg_flops * (3.0 if f16 else 6.0 if bf16 else (0.75 if g3m else 1.0))
     peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     achieved = exe_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     alg_rate = alg_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
-    if bf16:
+    if f16:
+        pmc_b = _profile_json("pmc_gemm_f16_r02.json", args.config)
+        pmc_t = pmc_b
+        kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_f16: every f32 operand scaled by a power of two "
+                 "(operand max from its producer sweep) and split into 2 f16 terms, 3 term products kept, f32 "
+                 "accumulation; 4 real products per complex product)")
+        exe_def = "executed f16 MFMA flops per launch (4 real products x 3 term products = 24*M*N*K) / avg launch time"
+    elif bf16:
         pmc_b = _profile_json("pmc_gemm_bf16_r02.json", args.config)
         pmc_t = pmc_b
         kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_bf16: every f32 operand split exactly into "
@@ -381,11 +389,13 @@ def main():
             res["cpu_baseline"] = cpu_baseline(args.config)
         except Exception as e:  # the baseline must never hide the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
-    if world == 1 and rank == 0 and bf16 and not args.no_alt:
-        try:
-            res["alt_f32_mfma"] = alt_f32(args)
-        except Exception as e:  # the alternate line must never hide the headline
-            res["alt_f32_mfma"] = {"error": repr(e)}
+    if world == 1 and rank == 0 and f16 and not args.no_alt:
+        for key, var, desc in (("alt_bf16_split", "TQ_GEMM_F16", "bf16 3-term split, v_mfma_f32_32x32x16_bf16"),
+                               ("alt_f32_mfma", "TQ_GEMM_BF16", "v_mfma_f32_32x32x2_f32")):
+            try:
+                res[key] = alt_gemm(args, var, desc)
+            except Exception as e:  # the alternate lines must never hide the headline
+                res[key] = {"error": repr(e)}
     if world == 1 and rank == 0 and not args.no_c5:
         try:
             res["c5_train"] = c5_train(dev, with_cpu=not args.no_cpu_baseline)

@@ -95,7 +95,11 @@ int permute_launch(int dtype, int rank, const int64_t* shape, const int64_t* src
 int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
                 const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
-                void* workspace, size_t ws_bytes, hipStream_t stream);
+                void* workspace, size_t ws_bytes, hipStream_t stream,
+                const uint32_t* amax_a = nullptr, const uint32_t* amax_b = nullptr);
+// amax_a / amax_b (optional, complex64): float bits of max |re|, |im| over A / B, written by the
+// operands' producers (plan: the sweep ops that store them); the f16-split kernel then skips its
+// own max pre-pass over A and B
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
 // apply a small operand along (at most two runs of) contracted modes (tq_apply.hip):
 //   C[o][n][m][i] = sum_{k1,k2} S[o][k1][m][k2][i] * G[k1*K2+k2][n]   (S, C, G contiguous)

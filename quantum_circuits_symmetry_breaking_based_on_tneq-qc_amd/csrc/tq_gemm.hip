@@ -388,7 +388,8 @@ struct FastArgs {
   int64_t kchunk;  // K per split (multiple of BK)
   int mt, nt, splits, batch;
   float beta;
-  const uint32_t* amax;  // f16 split kernel: max |x| bits of A and B (absmax_kouter_kernel)
+  const uint32_t* amax_a;  // f16 split kernel: max |x| bits of A / B (producer or absmax pre-pass)
+  const uint32_t* amax_b;
 };
 
 template <int N>
@@ -700,8 +701,16 @@ __device__ __forceinline__ void st_lds(char* p, const uint32_t (&w)[N / 2]) {
   else *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
 }
 
-// byte offset of (row, k-half) inside a term plane
-__device__ __forceinline__ int swz(int row, int kh) { return row * 32 + ((kh ^ ((row >> 3) & 1)) << 4); }
+// byte offset of (row, k-half) inside a term plane: rows of 32 B; on every other group of 8 rows
+// the two 16-B k-halves are swapped, and rows 2i / 2i+1 trade places where row bit 2 is set.
+// ds_read_b128 (bank = byte/4 mod 64, lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, +32):
+// a group's 16 rows land on 16 distinct (row mod 8, half) slots; ds_write_b64 (bank = byte/4
+// mod 32, 16 contiguous lanes): the staging stores of a group — rows 2r or 2r+1, r = 4q..4q+3,
+// x four 8-B k-groups — land on 4 distinct 32-B blocks mod 128 B (PMC SQ_LDS_BANK_CONFLICT 0;
+// without the row swap, rows 2r and 2r+4 were 2-way on every store)
+__device__ __forceinline__ int swz(int row, int kh) {
+  return (row ^ ((row >> 2) & 1)) * 32 + ((kh ^ ((row >> 3) & 1)) << 4);
+}
 // sign flip of 8 packed 16-bit floats (bf16 and f16 keep the sign in bit 15)
 __device__ __forceinline__ uint4 neg8(uint4 v) {
   return make_uint4(v.x ^ 0x80008000u, v.y ^ 0x80008000u, v.z ^ 0x80008000u, v.w ^ 0x80008000u);
@@ -775,8 +784,8 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   // power-of-two operand scales (f16 terms): from the operands' max |x| (absmax_kouter_kernel)
   int sca = 0, scb = 0;
   if constexpr (SP::SCALED) {
-    sca = scale_exp(g.amax[0]);
-    scb = scale_exp(g.amax[1]);
+    sca = scale_exp(*g.amax_a);
+    scb = scale_exp(*g.amax_b);
   }
 
   // staging registers, NSET sets (K-step mod NSET).  Threads 0 .. NT/2-1 stage A, the rest B
@@ -1244,7 +1253,7 @@ template <typename R, bool CPLX>
 int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
                  const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB,
                  double beta, void* C, int64_t ldc, int64_t sC, void* W, size_t wsb,
-                 hipStream_t stream) {
+                 hipStream_t stream, const uint32_t* amax_a, const uint32_t* amax_b) {
   using C_ = Cfg<R, CPLX>;
   constexpr int EW = CPLX ? 2 : 1;
   constexpr int VE = 16 / (EW * (int)sizeof(R));
@@ -1269,16 +1278,23 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
         const int64_t nb = (int64_t)f.mt * f.nt * fs * batch;
         // the f16 split needs the two max words behind the split-K slabs
         const size_t slab = fs > 1 ? need : 0;
-        if (gemm_f16() && W != nullptr && wsb >= slab + kAmaxBytes) {
-          uint32_t* amax = reinterpret_cast<uint32_t*>(static_cast<char*>(W) + slab);
-          TQ_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), stream));
-          const int64_t rows = K * batch;
-          const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1024));
-          hipLaunchKernelGGL(xbf::absmax_kouter_kernel, dim3(gx, 2), dim3(256), 0, stream,
-                             (const float4*)A, lda / 2, sA / 2, (const float4*)B, ldb / 2, sB / 2, K,
-                             M / 2, N / 2, batch, amax);
-          TQ_HIP(hipGetLastError());
-          f.amax = amax;
+        const bool ext = amax_a != nullptr && amax_b != nullptr;
+        if (gemm_f16() && (ext || (W != nullptr && wsb >= slab + kAmaxBytes))) {
+          if (ext) {
+            f.amax_a = amax_a;
+            f.amax_b = amax_b;
+          } else {
+            uint32_t* amax = reinterpret_cast<uint32_t*>(static_cast<char*>(W) + slab);
+            TQ_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), stream));
+            const int64_t rows = K * batch;
+            const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1024));
+            hipLaunchKernelGGL(xbf::absmax_kouter_kernel, dim3(gx, 2), dim3(256), 0, stream,
+                               (const float4*)A, lda / 2, sA / 2, (const float4*)B, ldb / 2, sB / 2, K,
+                               M / 2, N / 2, batch, amax);
+            TQ_HIP(hipGetLastError());
+            f.amax_a = amax;
+            f.amax_b = amax + 1;
+          }
           hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitF16>), dim3((unsigned)nb),
                              dim3(xbf::TileH::NT), 0, stream, f);
         } else {
@@ -1433,7 +1449,8 @@ size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch)
 int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
                 const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
-                void* workspace, size_t ws_bytes, hipStream_t stream) {
+                void* workspace, size_t ws_bytes, hipStream_t stream, const uint32_t* amax_a,
+                const uint32_t* amax_b) {
   TQ_CHECK_ARG(dtype_valid(dtype), "dtype");
   TQ_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "negative size");
   TQ_CHECK_ARG(transA == 0 || transA == 1, "transA");
@@ -1445,16 +1462,16 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
   switch (dtype) {
     case TQ_F32:
       return launch_typed<float, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
     case TQ_C64:
       return launch_typed<float, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
     case TQ_F64:
       return launch_typed<double, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
     case TQ_C128:
       return launch_typed<double, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream);
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
   }
   return TQ_ERR_INVALID;
 }

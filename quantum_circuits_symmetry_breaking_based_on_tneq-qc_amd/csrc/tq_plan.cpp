@@ -239,6 +239,7 @@ class Compiler {
         for (auto& g : op.sgates) fix(g.g);
       }
     }
+    assign_amax();
     // table layout
     size_t tb = 0;
     P_.perm_tab_off.clear();
@@ -256,6 +257,8 @@ class Compiler {
       P_.stab_off.push_back(tb);
       tb += (b.size() + kAlign - 1) / kAlign * kAlign;
     }
+    P_.amax_off = tb;
+    tb += ((size_t)(P_.n_amax_once + P_.n_amax_slice) * sizeof(uint32_t) + kAlign - 1) / kAlign * kAlign;
     P_.table_bytes = tb;
     for (auto& op : P_.ops) {
       (op.invariant ? P_.flops_once : P_.flops_slice) += op.flops;
@@ -282,6 +285,67 @@ class Compiler {
       }
     P_.describe = d.str();
     return TQ_OK;
+  }
+
+  // Operand-max words for the complex64 f16-split GEMM (tq_gemm.hip): when a GEMM that can take
+  // the K-outer fast path reads an operand that one sweep2 op stored in full (same buffer, same
+  // element count, no other writer in between), that sweep op max-es |re|, |im| of what it
+  // stores into a word the GEMM reads, instead of the GEMM re-reading both operands (1 GiB per
+  // C4 slice) for their max.  Words of slice-invariant producers are zeroed once per execute
+  // call, the others before every slice.
+  void assign_amax() {
+    P_.n_amax_once = P_.n_amax_slice = 0;
+    if (P_.dtype != TQ_C64) return;
+    const int64_t esz = (int64_t)P_.esz;
+    auto span = [&](const BufRef& b, int64_t n, int* space, int64_t* lo, int64_t* hi) {
+      if (b.kind == BUF_ARENA) { *space = 0; *lo = b.off * esz; }
+      else if (b.kind == BUF_PINNED) { *space = 0; *lo = (int64_t)P_.pinned_base + b.off * esz; }
+      else if (b.kind == BUF_OUTPUT) { *space = 1; *lo = b.off * esz; }
+      else return false;
+      *hi = *lo + n * esz;
+      return true;
+    };
+    std::vector<int> once, slice;  // producer op indices, in word order
+    auto producer = [&](int gi, const BufRef& r, int64_t n) -> int {
+      int sp, spw;
+      int64_t lo, hi, wlo, whi;
+      if (!span(r, n, &sp, &lo, &hi)) return -1;
+      for (int j = gi - 1; j >= 0; --j) {
+        const Op& w = P_.ops[j];
+        if (!span(w.c, w.nc, &spw, &wlo, &whi)) continue;
+        if (spw != sp || whi <= lo || hi <= wlo) continue;
+        // the latest writer of these bytes: usable only if it stored exactly this operand
+        if (w.kind == OP_SWEEP2 && !w.writes_output && wlo == lo && whi == hi) return j;
+        return -1;
+      }
+      return -1;
+    };
+    std::vector<int> prod_a(P_.ops.size(), -1), prod_b(P_.ops.size(), -1);
+    for (size_t i = 0; i < P_.ops.size(); ++i) {
+      const Op& g = P_.ops[i];
+      if (g.kind != OP_GEMM || g.transA != 1 || g.transB != 0) continue;
+      if (g.M % 128 || g.N % 128 || g.K % 16 || g.lda % 2 || g.ldb % 2) continue;
+      if (g.lda >= (int64_t(1) << 24) || g.ldb >= (int64_t(1) << 24)) continue;
+      if (g.batch > 1 && (g.sA % 2 || g.sB % 2)) continue;
+      const int pa = producer((int)i, g.a, g.na), pb = producer((int)i, g.b, g.nb);
+      if (pa < 0 || pb < 0) continue;
+      prod_a[i] = pa;
+      prod_b[i] = pb;
+      for (int j : {pa, pb}) {
+        auto& v = P_.ops[j].invariant ? once : slice;
+        if (std::find(v.begin(), v.end(), j) == v.end()) v.push_back(j);
+      }
+    }
+    P_.n_amax_once = (int)once.size();
+    P_.n_amax_slice = (int)slice.size();
+    for (size_t q = 0; q < once.size(); ++q) P_.ops[once[q]].amax_word = (int)q;
+    for (size_t q = 0; q < slice.size(); ++q) P_.ops[slice[q]].amax_word = P_.n_amax_once + (int)q;
+    for (size_t i = 0; i < P_.ops.size(); ++i) {
+      if (prod_a[i] < 0) continue;
+      P_.ops[i].amax_a = P_.ops[prod_a[i]].amax_word;
+      P_.ops[i].amax_b = P_.ops[prod_b[i]].amax_word;
+      P_.ops[i].note += " amax<-op" + std::to_string(prod_a[i]) + ",op" + std::to_string(prod_b[i]);
+    }
   }
 
   // Launch schedule.  Ops of one set (slice-invariant / per slice) are ordered by dependency
@@ -1705,6 +1769,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       return nullptr;
     };
     const double beta_out = first ? 0.0 : 1.0;
+    auto amax_word = [&](int w) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.amax_off) + w; };
     auto launch_one = [&](const Op& op, hipStream_t st) -> int {
       const double beta = op.writes_output ? beta_out : 0.0;
       switch (op.kind) {
@@ -1715,7 +1780,9 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
         case OP_GEMM:
           TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
                              op.lda, op.sA, ptr(op.b), op.ldb, op.sB, beta, ptr(op.c), op.ldc, op.sC,
-                             op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, st));
+                             op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, st,
+                             op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
+                             op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr));
           break;
         case OP_APPLY:
           TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.M, op.K2, op.I, op.N, ptr(op.a), ptr(op.b),
@@ -1827,6 +1894,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           blocks += o.nblocks;
           o.beta = op.writes_output ? beta_out : 0.0;
           o.use_beta = o.beta != 0.0;
+          o.amax = op.amax_word >= 0 ? amax_word(op.amax_word) : nullptr;
         }
         TQ_TRY(sweep2_launch(P.dtype, L, stream));
       } else {
@@ -1838,8 +1906,12 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       }
       return TQ_OK;
     };
-    if (sl == s_begin)
+    if (sl == s_begin) {
+      if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
       for (auto& grp : P.sched_once) TQ_TRY(launch(grp));
+    }
+    if (P.n_amax_slice)
+      TQ_HIP(hipMemsetAsync(amax_word(P.n_amax_once), 0, P.n_amax_slice * sizeof(uint32_t), stream));
     for (auto& grp : P.sched_slice) TQ_TRY(launch(grp));
     first = false;
   }

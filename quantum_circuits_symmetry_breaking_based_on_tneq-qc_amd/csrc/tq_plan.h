@@ -64,6 +64,9 @@ struct Op {
   int load_colfast = 1, store_colfast = 1;
   // sweep2: descriptor blob = stabs[stab] (an S2Desc), launched with s2_blocks(s2_nchunks)
   int64_t s2_nchunks = 0;
+  // operand-max words (complex64 f16-split GEMM): a sweep2 op that produces a GEMM operand
+  // max-es its stored values into word amax_word; the GEMM reads words amax_a / amax_b
+  int amax_word = -1, amax_a = -1, amax_b = -1;
   // element counts of a / b / c / ws (hazard analysis of the launch schedule)
   int64_t na = 0, nb = 0, nc = 0, nws = 0;
   // bookkeeping
@@ -98,6 +101,10 @@ struct Plan {
   std::vector<std::vector<char>> stabs;     // OP_SWEEP table blobs
   std::vector<size_t> stab_off;
   size_t table_bytes = 0;
+  // operand-max words behind the tables (zeroed per execute call: the first n_amax_once, written
+  // by slice-invariant producers; per slice: the next n_amax_slice)
+  size_t amax_off = 0;
+  int n_amax_once = 0, n_amax_slice = 0;
   size_t arena_bytes = 0;
   size_t pinned_base = 0;             // pinned (hoisted, slice-invariant) results live above this
   void* d_arena = nullptr;

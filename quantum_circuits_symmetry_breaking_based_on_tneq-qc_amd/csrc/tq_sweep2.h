@@ -93,6 +93,9 @@ struct S2Op {
   int block_begin = 0, nblocks = 0;
   double beta = 0.0;
   int use_beta = 0, pad = 0;
+  // complex64 only, optional: the op atomically max-es the float bits of max |re|, |im| over
+  // every value it stores into *amax (zeroed before; the max a consuming f16-split GEMM scales by)
+  uint32_t* amax = nullptr;
 };
 
 struct S2Launch {

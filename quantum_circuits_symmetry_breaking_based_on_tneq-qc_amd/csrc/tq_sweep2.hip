@@ -395,6 +395,14 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   const int rin = (nin + NT - 1) / NT, rout = (nout + NT - 1) / NT;  // slots in use (powers of 2)
   const bool use_beta = op.use_beta;
   const double beta = op.beta;
+  // producer-side max of a complex64 GEMM operand (S2Op::amax): max |re|, |im| of the values
+  // this thread stores, one atomic per wave after the chunk loop
+  constexpr bool kC64 = std::is_same<T, c64>::value;
+  uint32_t* const amax = kC64 ? op.amax : nullptr;
+  float vmax = 0.f;
+  auto track = [&](const T& v) {
+    if constexpr (kC64) vmax = fmaxf(vmax, fmaxf(fabsf(v.re), fabsf(v.im)));
+  };
   __syncthreads();
   TQ_TS(1);
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
@@ -568,34 +576,48 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     const int64_t base = base_out(i, ch);
     // the tile leaves LDS in batches of 4 register slots, each batch stored before the next is
     // read (keeps the register budget)
-    if (rout >= 4) {
-      for (int r0 = 0; r0 < rout; r0 += 4) {
-        T t[4];
+    auto store_chunk = [&](auto tracked) {
+      constexpr bool TRK = decltype(tracked)::value;
+      if (rout >= 4) {
+        for (int r0 = 0; r0 < rout; r0 += 4) {
+          T t[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ hot.st_ha[r0 + q]];
-        if (st_lane) {
+          for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ hot.st_ha[r0 + q]];
+          if (st_lane) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + q]), sto);
-            *p = use_beta ? scale_add(t[q], *p, beta) : t[q];
+            for (int q = 0; q < 4; ++q) {
+              T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + q]), sto);
+              const T v = use_beta ? scale_add(t[q], *p, beta) : t[q];
+              *p = v;
+              if constexpr (TRK) track(v);
+            }
           }
+          asm volatile("" ::: "memory");
         }
-        asm volatile("" ::: "memory");
+      } else {
+        T t[4];
+        TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ hot.st_ha[r]]);
+        if (st_lane) {
+          TQ_BY_COUNT(4, rout, {
+            T* p = lane_at(Y + uniform(base + hot.st_hm[r]), sto);
+            const T v = use_beta ? scale_add(t[r], *p, beta) : t[r];
+            *p = v;
+            if constexpr (TRK) track(v);
+          });
+        }
       }
-    } else {
-      T t[4];
-      TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ hot.st_ha[r]]);
-      if (st_lane) {
-        TQ_BY_COUNT(4, rout, {
-          T* p = lane_at(Y + uniform(base + hot.st_hm[r]), sto);
-          *p = use_beta ? scale_add(t[r], *p, beta) : t[r];
-        });
-      }
-    }
+    };
+    if (kC64 && amax) store_chunk(std::true_type{});
+    else store_chunk(std::false_type{});
     __syncthreads();  // every wave has read the tile
     if (ch == lb) TQ_TS(5);
     if (more) fill(i + 1, nxt);
     __syncthreads();
+  }
+  if (amax) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(vmax));
   }
 #ifdef TQ_S2_TIMING
   __builtin_amdgcn_s_waitcnt(0);

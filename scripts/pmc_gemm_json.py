@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
-"""Summarize the PMC passes of scripts/pmc_gemm_bf16.sh into profiles/pmc_gemm_bf16_r02.json:
-MFMA busy fraction of the bf16-split boundary GEMM (SQ_VALU_MFMA_BUSY_CYCLES advances 32 cycles
-per v_mfma_f32_32x32x16_bf16), the effective shader clock (GRBM_GUI_ACTIVE summed over the 8
+"""Summarize the PMC passes of scripts/pmc_gemm_bf16.sh (or pmc_gemm_f16.sh: 4th argument "f16")
+into profiles/pmc_gemm_{bf16,f16}_r02.json: MFMA busy fraction of the split boundary GEMM
+(SQ_VALU_MFMA_BUSY_CYCLES advances 32 cycles per v_mfma_f32_32x32x16_bf16 / _f16), the effective shader clock (GRBM_GUI_ACTIVE summed over the 8
 XCDs / kernel duration), and HBM bytes per launch (FETCH_SIZE doubled per the gfx950 correction
 in MI355X_MICROARCH.md's HBM section, + WRITE_SIZE)."""
 import collections, csv, json, sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_gemm_bf16_r02.json"
-frag = "gemm_c64_kouter_bf16"
+kind = sys.argv[3] if len(sys.argv) > 3 else "bf16"
+F16 = kind == "f16"
+frag = "SplitF16" if F16 else "SplitBF16"
+pre = "pmcf" if F16 else "pmcx"
+kt = "ktf" if F16 else "ktx"
 
 
 def passes(d):
@@ -22,22 +26,24 @@ def passes(d):
     return {k: sum(v) / len(v) for k, v in agg.items()}, len(n)
 
 
-c1, n1 = passes("pmcx1")
-c2, _ = passes("pmcx2")
-c3, _ = passes("pmcx3")
+c1, n1 = passes(pre + "1")
+c2, _ = passes(pre + "2")
+c3, _ = passes(pre + "3")
 # kernel duration from the kernel-trace pass (same command, no counters)
-dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(f"{root}/ktx/run_kernel_trace.csv"))
+dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(f"{root}/{kt}/run_kernel_trace.csv"))
        if frag in r["Kernel_Name"]]
 avg_ns = sum(dur) / len(dur)
 M = N = 1024
 K = 65536
-n_mfma = 24 * (M // 32) * (N // 32) * (K // 16)      # 4M x 6 split products per 32x32x16 tile-step
+n_mfma = (12 if F16 else 24) * (M // 32) * (N // 32) * (K // 16)  # 4M x (3 | 6) term products per tile-step
 cyc_xcd = c1["GRBM_GUI_ACTIVE"] / 8
 res = {
     "config": "C4",
-    "kernel": "gemm_c64_kouter_bf16_kernel<Tile<2,4,2,1>> (complex64 via exact 3-term bf16 split, 4M, "
-              "M=N=1024, K=65536 per slice, block 128x128, split-K 4)",
-    "command": "scripts/pmc_gemm_bf16.sh (rocprofv3 --pmc ... --kernel-include-regex gemm_c64 -- python3 bench.py "
+    "kernel": ("gemm_c64_kouter_split_kernel<TileH, SplitF16> (complex64 via 2-term f16 split of the "
+               "power-of-two-scaled operands, 4M, " if F16 else
+               "gemm_c64_kouter_split_kernel<TileX, SplitBF16> (complex64 via exact 3-term bf16 split, 4M, ")
+              + "M=N=1024, K=65536 per slice, block 128x128, split-K 4)",
+    "command": f"scripts/pmc_gemm_{kind}.sh (rocprofv3 --pmc ... --kernel-include-regex gemm_c64 -- python3 bench.py "
                "--no-cpu-baseline --no-c5 --steps 2 --warmup 1; FETCH_SIZE and WRITE_SIZE in separate passes; "
                "durations from a --kernel-trace pass)",
     "launches": n1,

@@ -96,6 +96,21 @@ def test_native_plan_c4_structure():
     assert p.query("flops") == pytest.approx(p.query("flops_once") + 8 * p.query("flops_slice"), rel=1e-6)
 
 
+def test_c4_gemm_operand_max_comes_from_its_producers():
+    """The C4 boundary GEMM (complex64, K-outer fast path) reads both operands' max |x| from the
+    per-slice sweep ops that store them (csrc/tq_plan.cpp assign_amax), not from a pre-pass."""
+    import re
+    e, p = _plan(config_task("C4"))
+    d = p.describe().splitlines()
+    ops = [l for l in d if l.startswith("[once]") or l.startswith("[slice]")]
+    gemm = [l for l in ops if "GEMM" in l]
+    m = re.search(r"amax<-op(\d+),op(\d+)", gemm[0])
+    assert m, gemm[0]
+    for j in (int(m.group(1)), int(m.group(2))):
+        assert "SWEEP2" in ops[j] and ops[j].startswith("[slice]")
+        assert ops.index(gemm[0]) > j
+
+
 def _schedule(d):
     once, per = [], []
     for l in d:
