@@ -573,51 +573,63 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_kernel(FastArgs g) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// complex64 on the bf16 matrix cores with f32 accuracy (default K-outer complex64 fast path;
-// TQ_GEMM_BF16=0 selects the f32-MFMA kernel above).
+// complex64 on the 16-bit matrix cores with f32 accuracy (the K-outer complex64 fast path;
+// TQ_GEMM_BF16=0 selects the f32-MFMA kernel above).  Every f32 operand value is split into
+// 16-bit terms and each real product a*b becomes a few term products on the MFMA, accumulated
+// in f32; the complex product is the 4-multiplication form (Cr += Ar Br + (-Ai) Bi,
+// Ci += Ar Bi + Ai Br; -Ai by flipping the fragment's sign bits).  Two splits (SplitF16 /
+// SplitBF16 below):
+//  * f16 (default): x * 2^sc (sc from the operand's max |x|, so max |x| 2^sc is in [2^14, 2^15))
+//    = h + l, two f16 terms good to 2^-24 relative; 3 term products (hh, hl, lh) = 12
+//    v_mfma_f32_32x32x16_f16 per 32 x 32 x 16 complex tile-step.  The max comes from the operand's
+//    producer (plan: the sweep op that stores it) or from a pre-pass (absmax_kouter_kernel).
+//  * bf16 (TQ_GEMM_F16=0): x = h + m + l exactly by truncation, 6 term products = 24 MFMAs.
+// Both run at the same cycles per MFMA, so the f16 split halves the MFMA work.
 //
-// Split: every f32 value x is split EXACTLY into three bf16 terms by truncation, h = x with the
-// low 16 bits cleared, r = x - h (exact, <= 16 significant bits), m = r truncated the same way,
-// l = r - m (exact, <= 8 significant bits, a bf16 with no rounding): x == h + m + l.  A real
-// product a*b keeps the six terms down to 2^-16 relative (hh, hm, mh, hl, lh, mm; the dropped
-// ml, lm, ll are <= 2^-24 relative, below the f32 product's own rounding), each one
-// v_mfma_f32_32x32x16_bf16 accumulating in f32.  The complex product is the 4-multiplication
-// form (Cr += Ar Br + (-Ai) Bi, Ci += Ar Bi + Ai Br; -Ai by flipping the fragment's sign bits):
-// 24 bf16 MFMAs of 32 cycles per 32 x 32 x 16 complex tile-step against 4 x 8 f32 MFMAs of 64
-// (2.67x fewer MFMA cycles).  Measured alternatives at the C4 shape (1024 x 1024 x 65536, r02):
-// this kernel 2.61-2.63 ms; the same with Gauss 3M (18 MFMAs, a third split plane re + im)
-// 2.52 ms with one wave per SIMD; split into bf16 term planes by a separate HBM pass and
-// streamed by LDS-DMA 2.35-2.7 ms + 0.32 ms per operand split (fill-bound: 18 B per element);
-// the f32-MFMA kernel 3.35 ms.  The clock runs at ~1.9 GHz under this load (PMC GRBM_GUI_ACTIVE),
-// where the 24-MFMA floor is 1.66 ms; what is left is the per-K-step barrier and in-order issue
-// (MFMA busy 62-64 %).
+// Data path per K-step of 16 (block 128 x 128, one barrier per step): half of the threads stage
+// A, half B; a thread owns 2 rows x 4 (8) consecutive k and loads them as 16-B vectors (one
+// complex pair per k) with an SGPR base + 32-bit lane offset, NSET - 1 steps ahead, into
+// register sets; the split of step t + 1 goes into the other half of a double-buffered LDS image
+// of term planes (2 x NTERM planes of [row][16 k] 16-bit values, 32-B rows, swizzled: swz) while
+// the MFMAs of step t run from fragments read at the start of the step (one ds_read_b128 each, in
+// the order the MFMA pairs first use them).  The f16 kernel tells the scheduler to interleave the
+// split with the MFMAs (sched_group_barrier).
 //
-// Data path per K-step of 16: each thread loads KPT complex values (consecutive k of one row) of
-// A and of B straight into registers one K-step ahead of their split (two register sets, the
-// loop is unrolled by two), and splits them into the other half of a double-buffered LDS image
-// while this step's MFMAs run: 2 planes x 3 terms.  The MFMA fragment of lane (row r, k-half h)
-// is one ds_read_b128; term-plane rows are 32 B (16 k) and the two 16-B k-halves of a row are
-// swapped on every other group of 8 rows, which makes every 16-lane group of a fragment read hit
-// 16 distinct bank slots (PMC SQ_LDS_BANK_CONFLICT = 0).  One barrier per K-step.
+// Measured at the C4 shape (1024 x 1024 x 65536, split-K 4; r02): f16 1.40-1.43 ms, MFMA busy
+// 62 % at the 1.77 GHz the chip holds (PMC); bf16 2.49 ms.  Steps that mattered: 16-B staging
+// loads instead of 8-B (the per-CU L2 request rate bounded the 8-B version: a loads-only variant
+// took as long as the whole kernel), the producer-side operand max instead of a 1-GiB pre-pass
+// (0.23 ms per launch).  Within 2-3 %: 3 vs 4 staging sets, one wave per SIMD with 64 x 64 wave
+// tiles (TileH4), the interleave, fragment-read order, a conflict-free store swizzle.  With the
+// MFMAs removed the kernel takes 0.66 ms at 2.3 GHz; with the loads removed 1.30 ms: the split
+// and the MFMAs overlap only partly.
 namespace xbf {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_> struct Tile {
+template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_> struct Tile {
+  // ILV: the scheduler is told to interleave the split (VALU, LDS stores) with the MFMAs
+  static constexpr bool ILV = ILV_;
   static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_, NTERM = NTERM_;
+  // staging register sets: a K-step's loads go out NSET - 1 steps before its split
+  static constexpr int NSET = NSET_;
   static constexpr int NW = WMW * WNW, NT = 64 * NW;
   static constexpr int WM = 32 * TI, WN = 32 * TJ, BM = WMW * WM, BN = WNW * WN, BK = 16;
   static constexpr int SUBA = BM * 32, SUBB = BN * 32;            // bytes per term plane
   static constexpr int BUF = 2 * NTERM * (SUBA + SUBB);           // 2 planes x NTERM terms, A and B
-  // one split task per thread and operand: KPT consecutive k of one row
+  // split task per thread: 2 rows x KPT consecutive k of one operand
   static constexpr int KPT = 16 * BM / NT;
   static_assert(BM == BN && (KPT == 4 || KPT == 8), "task split");
   static_assert(2 * BUF <= 160 * 1024, "LDS");
 };
 // 8 waves (two per SIMD) of 64 x 32, block 128 x 128, 64 accumulators per wave; 4-k split tasks
 // (ds_write_b64).  bf16: 3 terms, 2 x 48 KiB LDS; f16: 2 terms, 2 x 32 KiB.
-using TileX = Tile<2, 4, 2, 1, 3>;
-using TileH = Tile<2, 4, 2, 1, 2>;
+using TileX = Tile<2, 4, 2, 1, 3, 2, false>;   // bf16: 4 sets spill at 3 terms
+// f16 default: 8 waves (two per SIMD) of 64 x 32, block 128 x 128, 4 staging sets, interleaved
+using TileH = Tile<2, 4, 2, 1, 2, 4, true>;
+// f16 alternative (TQ_GEMM_F16_VAR=1): 4 waves (one per SIMD, 512 registers) of 64 x 64 — twice
+// the MFMAs per fragment read; measured within 2 % of the default
+using TileH4 = Tile<2, 2, 2, 2, 2, 4, true>;
 
 __device__ __forceinline__ uint32_t hi16(float x) { return __float_as_uint(x) & 0xffff0000u; }
 // pack the bf16 held in the high halves of two dwords: lo <- a, hi <- b
@@ -629,7 +641,6 @@ __device__ __forceinline__ uint32_t pk(uint32_t a, uint32_t b) { return __builti
 struct SplitBF16 {
   static constexpr int NTERM = 3, NPAIR = 6;
   static constexpr bool SCALED = false;
-  static constexpr int NSET = 2;  // staging register sets (4 spill at 3 terms)
   static constexpr int pa(int q) { return q == 0 ? 1 : q == 2 ? 2 : q == 4 ? 1 : 0; }  // 1 0 2 0 1 0
   static constexpr int pb(int q) { return q == 0 ? 1 : q == 1 ? 2 : q == 3 ? 1 : 0; }  // 1 2 0 1 0 0
   template <int N>
@@ -662,7 +673,6 @@ struct SplitBF16 {
 struct SplitF16 {
   static constexpr int NTERM = 2, NPAIR = 3;
   static constexpr bool SCALED = true;
-  static constexpr int NSET = 4;
   static constexpr int pa(int q) { return q == 0 ? 1 : 0; }  // 1 0 0
   static constexpr int pb(int q) { return q == 1 ? 1 : 0; }  // 0 1 0
   // per pair of values: 2 v_ldexp_f32, v_cvt_pk_f16_f32 (h), 2 v_fma_mix_f32 (r = x - h, reading
@@ -685,6 +695,20 @@ struct SplitF16 {
   static __device__ __forceinline__ f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
   }
+};
+
+// scheduling pattern (sched_group_barrier, one scheduling region): MFMA i, then up to V VALU,
+// and one LDS store after every E-th MFMA
+template <int I, int NM, int V, int E> struct Interleave {
+  static __device__ __forceinline__ void run() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+    if constexpr (I % E == E - 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    Interleave<I + 1, NM, V, E>::run();
+  }
+};
+template <int NM, int V, int E> struct Interleave<NM, NM, V, E> {
+  static __device__ __forceinline__ void run() {}
 };
 
 // exponent sc with max|x| * 2^sc in [2^14, 2^15) from the bits of max|x| (0 -> 0; inf/nan -> 0)
@@ -795,11 +819,11 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   // writes rows 0, 2, 4, 6 (+8..) x 32 B: distinct banks).  Per-CU L2 -> L1 request concurrency,
   // not bandwidth, bounded the 8-B-per-lane version (512 B per wave-load): ~7.5 B/clk/CU with the
   // MFMAs removed.  A K-step's loads are issued NSET - 1 K-steps before its split.
-  constexpr int KPT = 4, NSET = SP::NSET;
-  static_assert(TL::NT == 4 * BM && BM == BN, "two operands x BM/2 row pairs x 4 k-groups");
+  constexpr int KPT = TL::KPT, KG = 16 / KPT, NSET = TL::NSET;
+  static_assert(BM == BN && (TL::NT / 2) * 2 * KPT == BM * 16, "two operands x BM/2 row pairs x KG k-groups");
   const int op = __builtin_amdgcn_readfirstlane(tid >= TL::NT / 2 ? 1 : 0);  // wave-uniform: SGPR
   const int ot = tid & (TL::NT / 2 - 1);
-  const int trow = 2 * (ot >> 2), tkg = ot & 3;
+  const int trow = 2 * (ot / KG), tkg = ot % KG;
   float4 rv[NSET][KPT];
   // wave-uniform K-step base (SGPR pair) + per-lane 32-bit byte offsets fixed over the loop (no
   // per-step address VALU; launch: lda, ldb < 2^24 complex)
@@ -861,13 +885,29 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
 
   typedef uint4 FragA[2 * NTM][TI];
   typedef uint4 FragB[2 * NTM][TJ];
+  // planes in the order the MFMA pairs first use them (pair 0's four first), so the first MFMAs
+  // of a step wait for a third to a half of the step's fragment reads, not all of them
   auto read_frags = [&](const char* s, FragA& fa, FragB& fb) {
+    bool ra[NTM] = {}, rb[NTM] = {};
 #pragma unroll
-    for (int x = 0; x < 2 * NTM; ++x) {
+    for (int q = 0; q < SP::NPAIR; ++q) {
+      const int xa = SP::pa(q), xb = SP::pb(q);
+      if (!ra[xa]) {
+        ra[xa] = true;
 #pragma unroll
-      for (int i = 0; i < TI; ++i) fa[x][i] = *reinterpret_cast<const uint4*>(s + x * SUBA + a_off[i]);
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) fb[x][j] = *reinterpret_cast<const uint4*>(s + x * SUBB + b_off[j]);
+          for (int i = 0; i < TI; ++i)
+            fa[h * NTM + xa][i] = *reinterpret_cast<const uint4*>(s + (h * NTM + xa) * SUBA + a_off[i]);
+      }
+      if (!rb[xb]) {
+        rb[xb] = true;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            fb[h * NTM + xb][j] = *reinterpret_cast<const uint4*>(s + (h * NTM + xb) * SUBB + b_off[j]);
+      }
     }
   };
   // pairs of (A term, B term), smallest first
@@ -891,51 +931,69 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       }
   };
   // one steady-state K-step t (t + 1 < nkt, P = t mod NSET): loads of step t + NSET into the
-  // register set step t used (split one step ago) issued first, then the fragments of step t,
-  // the split of step t + 1 into the other LDS half, the MFMAs
+  // register set step t used (split one step ago) issued first; the split of step t + 1 into the
+  // other LDS half and the MFMAs of step t (fragments already in registers) interleave; after the
+  // barrier the fragments of step t + 1 are read, so they land under the next step's load issue
+  // and split instead of stalling its first MFMAs (one fragment set live at a time)
+  // body P (t = P mod U): register set P mod NSET, LDS half P & 1.  (Reading the next step's
+  // fragments right after the barrier, into a second fragment set, spilled at 256 registers and
+  // measured slower at 512 with fewer staging sets.)
+  FragA fa;
+  FragB fb;
   auto body = [&](auto par, int t) {
     constexpr int P = decltype(par)::value;
-    load(std::integral_constant<int, P>{}, t + NSET < nkt ? t + NSET : nkt - 1);
+    load(std::integral_constant<int, P % NSET>{}, t + NSET < nkt ? t + NSET : nkt - 1);
     __builtin_amdgcn_sched_barrier(0);
-    FragA fa;
-    FragB fb;
     read_frags(lds + (P & 1) * BUF, fa, fb);
     store_stage(std::integral_constant<int, (P + 1) % NSET>{}, (P & 1) ^ 1);
     mfmas(fa, fb);
+    if constexpr (TL::ILV) {
+      // fragment reads first, then every MFMA followed by up to 3 VALU (the split, the sign
+      // flips), the split's LDS stores spread evenly: without this the compiler issued the split
+      // and the MFMAs largely back to back (the no-MFMA variant's time added to the MFMA time)
+      constexpr int NM = SP::NPAIR * TI * TJ * 4;
+      constexpr int NR = 2 * NTM * (TI + TJ);
+      constexpr int NWR = 2 * 2 * NTM;  // LDS stores per thread: 2 rows x (re, im) x terms
+      __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+      Interleave<0, NM, 3, (NM / NWR > 0 ? NM / NWR : 1)>::run();
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the MFMAs of step t stay above the barrier
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
 
-  static_assert(NSET == 2 || NSET == 4, "unrolled by NSET below");
+  static_assert(NSET >= 2 && NSET <= 4, "register sets");
+  constexpr int U = NSET == 3 ? 6 : NSET;  // unroll: a multiple of NSET and of 2 (LDS halves)
   load(std::integral_constant<int, 0>{}, 0);
   load(std::integral_constant<int, 1>{}, nkt > 1 ? 1 : nkt - 1);
-  if constexpr (NSET == 4) {
-    load(std::integral_constant<int, NSET == 4 ? 2 : 0>{}, nkt > 2 ? 2 : nkt - 1);
-    load(std::integral_constant<int, NSET == 4 ? 3 : 0>{}, nkt > 3 ? 3 : nkt - 1);
-  }
+  if constexpr (NSET >= 3) load(std::integral_constant<int, NSET >= 3 ? 2 : 0>{}, nkt > 2 ? 2 : nkt - 1);
+  if constexpr (NSET >= 4) load(std::integral_constant<int, NSET >= 4 ? 3 : 0>{}, nkt > 3 ? 3 : nkt - 1);
   store_stage(std::integral_constant<int, 0>{}, 0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   int t = 0;
-  for (; t + NSET < nkt; t += NSET) {
-    body(std::integral_constant<int, 0>{}, t);
-    body(std::integral_constant<int, 1>{}, t + 1);
-    if constexpr (NSET == 4) {
-      body(std::integral_constant<int, NSET == 4 ? 2 : 0>{}, t + 2);
-      body(std::integral_constant<int, NSET == 4 ? 3 : 0>{}, t + 3);
-    }
+  for (; t + U < nkt; t += U) {
+    body(I0{}, t);
+    body(I1{}, t + 1);
+    if constexpr (U >= 4) { body(I2{}, t + 2); body(I3{}, t + 3); }
+    if constexpr (U >= 6) { body(I4{}, t + 4); body(I5{}, t + 5); }
   }
-  // 1 .. NSET steps left: all but the last split their successor
-  if (t + 1 < nkt) body(std::integral_constant<int, 0>{}, t);
-  if constexpr (NSET == 4) {
-    if (t + 2 < nkt) body(std::integral_constant<int, 1>{}, t + 1);
-    if (t + 3 < nkt) body(std::integral_constant<int, NSET == 4 ? 2 : 0>{}, t + 2);
+  // 1 .. U steps left: all but the last split their successor
+  if (t + 1 < nkt) body(I0{}, t);
+  if constexpr (U >= 4) {
+    if (t + 2 < nkt) body(I1{}, t + 1);
+    if (t + 3 < nkt) body(I2{}, t + 2);
   }
-  t = nkt - 1;
-  {
-    FragA fa;
-    FragB fb;
-    read_frags(lds + (t & 1) * BUF, fa, fb);
-    mfmas(fa, fb);
+  if constexpr (U >= 6) {
+    if (t + 4 < nkt) body(I3{}, t + 3);
+    if (t + 5 < nkt) body(I4{}, t + 4);
   }
+  read_frags(lds + ((nkt - 1) & 1) * BUF, fa, fb);
+  mfmas(fa, fb);  // step nkt - 1
 
   const bool partial = g.splits > 1;
   float* Cout = partial ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * 2 : g.C + (int64_t)b * g.sC * 2;
@@ -1272,7 +1330,7 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;
       if (gemm_bf16()) {
         using TX = xbf::TileX;
-        static_assert(TX::BM == xbf::TileH::BM && TX::BN == xbf::TileH::BN, "same split-K tiling");
+        static_assert(TX::BM == xbf::TileH::BM && TX::BN == xbf::TileH::BN && TX::BM == xbf::TileH4::BM, "same split-K tiling");
         f.mt = (int)(M / TX::BM);
         f.nt = (int)(N / TX::BN);
         const int64_t nb = (int64_t)f.mt * f.nt * fs * batch;
@@ -1295,8 +1353,13 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.amax_a = amax;
             f.amax_b = amax + 1;
           }
-          hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitF16>), dim3((unsigned)nb),
-                             dim3(xbf::TileH::NT), 0, stream, f);
+          static const int var = [] { const char* e = getenv("TQ_GEMM_F16_VAR"); return e ? atoi(e) : 0; }();
+          if (var == 1)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH4, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH4::NT), 0, stream, f);
+          else
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH::NT), 0, stream, f);
         } else {
           hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<TX, xbf::SplitBF16>), dim3((unsigned)nb),
                              dim3(TX::NT), 0, stream, f);
