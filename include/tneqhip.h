@@ -65,12 +65,14 @@ int tq_device_synchronize(void);
 /* Library configuration: "gemm_bf16" (1: the K-outer complex64 GEMM runs on the 16-bit matrix
  * cores with f32 accuracy; env TQ_GEMM_BF16=0 selects the f32-MFMA kernel), "gemm_f16" (1, with
  * gemm_bf16: a 2-term f16 split of the power-of-two-scaled operands, 12 MFMAs per complex
- * tile-step; 0 / env TQ_GEMM_F16=0: an exact 3-term bf16 split, 24 MFMAs), "gemm_3m" (1: the f32-MFMA complex64 kernel uses Gauss's 3-multiplication
+ * tile-step; 0 / env TQ_GEMM_F16=0: an exact 3-term bf16 split, 24 MFMAs), "gemm_f16_var" (f16
+ * tile variant: 0 = 8 waves of 64x32, 1 = 4 waves of 64x64, 2 = 4 waves of 64x64 with Gauss's
+ * 3-multiplication product; env TQ_GEMM_F16_VAR), "gemm_3m" (1: the f32-MFMA complex64 kernel uses Gauss's 3-multiplication
  * product, env TQ_GEMM_3M=0 turns it off), "sweep" (fused multi-gate sweeps, env TQ_SWEEP),
  * "graphs" (plan execution through hipGraphs, env TQ_GRAPH).  -1 if unknown.  No reference
  * counterpart (the reference has no native layer); used for measurement reports. */
 int64_t tq_library_query(const char* key);
-/* Sets "gemm_bf16" / "gemm_f16" / "gemm_3m" at run time (launches issued afterwards; a plan replaying a
+/* Sets "gemm_bf16" / "gemm_f16" / "gemm_f16_var" / "gemm_3m" at run time (launches issued afterwards; a plan replaying a
  * captured hipGraph keeps the kernels it captured).  TQ_ERR_INVALID for other keys.  No
  * reference counterpart; used by tests and A/B measurements. */
 int tq_library_set(const char* key, int64_t value);

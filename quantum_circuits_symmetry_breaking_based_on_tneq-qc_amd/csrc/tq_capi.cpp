@@ -19,6 +19,7 @@ namespace tq {
 bool gemm_3m();
 bool gemm_bf16();
 bool gemm_f16();
+int gemm_f16_var();
 bool gemm_configure(const char* key, int64_t v);
 bool graphs_enabled();
 bool sweeps_enabled_global();
@@ -30,6 +31,7 @@ extern "C" int64_t tq_library_query(const char* key) {
   if (k == "gemm_3m") return tq::gemm_3m() ? 1 : 0;
   if (k == "gemm_bf16") return tq::gemm_bf16() ? 1 : 0;
   if (k == "gemm_f16") return tq::gemm_f16() ? 1 : 0;
+  if (k == "gemm_f16_var") return tq::gemm_f16_var();
   if (k == "graphs") return tq::graphs_enabled() ? 1 : 0;
   if (k == "sweep") return tq::sweeps_enabled_global() ? 1 : 0;
 

@@ -34,6 +34,14 @@ static int env_flag(const char* name) {
 static std::atomic<int> g_gemm_3m{env_flag("TQ_GEMM_3M")};
 static std::atomic<int> g_gemm_bf16{env_flag("TQ_GEMM_BF16")};
 static std::atomic<int> g_gemm_f16{env_flag("TQ_GEMM_F16")};
+static int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
+// f16-split tile variant: 0 = 8 waves of 64 x 32 (default), 1 = 4 waves of 64 x 64, 2 = 4 waves of
+// 64 x 64 with Gauss's 3-multiplication product (measurements: DESIGN.md §3)
+static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR")};
+int gemm_f16_var() { return g_gemm_f16_var.load(std::memory_order_relaxed); }
 bool gemm_3m() { return g_gemm_3m.load(std::memory_order_relaxed) != 0; }
 // The complex64 K-outer fast path runs on the bf16 matrix cores with an exact 3-term split of
 // every f32 operand (gemm_c64_kouter_split_kernel<TileX, SplitBF16>, f32 accuracy); TQ_GEMM_BF16=0 (or
@@ -50,6 +58,11 @@ bool gemm_configure(const char* key, int64_t v) {
   if (k == "gemm_3m") { g_gemm_3m = v ? 1 : 0; return true; }
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
+  if (k == "gemm_f16_var") {
+    if (v < 0 || v > 2) return false;
+    g_gemm_f16_var = (int)v;
+    return true;
+  }
   return false;
 }
 
@@ -607,16 +620,20 @@ namespace xbf {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_> struct Tile {
+template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_, bool G3_ = false>
+struct Tile {
   // ILV: the scheduler is told to interleave the split (VALU, LDS stores) with the MFMAs
   static constexpr bool ILV = ILV_;
+  // G3: Gauss's 3-multiplication product (planes re, im, re + im per term; 3 accumulator sets)
+  static constexpr bool G3 = G3_;
+  static constexpr int NGRP = G3_ ? 3 : 2;
   static constexpr int WMW = WMW_, WNW = WNW_, TI = TI_, TJ = TJ_, NTERM = NTERM_;
   // staging register sets: a K-step's loads go out NSET - 1 steps before its split
   static constexpr int NSET = NSET_;
   static constexpr int NW = WMW * WNW, NT = 64 * NW;
   static constexpr int WM = 32 * TI, WN = 32 * TJ, BM = WMW * WM, BN = WNW * WN, BK = 16;
   static constexpr int SUBA = BM * 32, SUBB = BN * 32;            // bytes per term plane
-  static constexpr int BUF = 2 * NTERM * (SUBA + SUBB);           // 2 planes x NTERM terms, A and B
+  static constexpr int BUF = NGRP * NTERM * (SUBA + SUBB);        // (re, im[, re+im]) x terms, A, B
   // split task per thread: 2 rows x KPT consecutive k of one operand
   static constexpr int KPT = 16 * BM / NT;
   static_assert(BM == BN && (KPT == 4 || KPT == 8), "task split");
@@ -630,6 +647,9 @@ using TileH = Tile<2, 4, 2, 1, 2, 4, true>;
 // f16 alternative (TQ_GEMM_F16_VAR=1): 4 waves (one per SIMD, 512 registers) of 64 x 64 — twice
 // the MFMAs per fragment read; measured within 2 % of the default
 using TileH4 = Tile<2, 2, 2, 2, 2, 4, true>;
+// f16, Gauss 3M (TQ_GEMM_F16_VAR=2): P1 = Ar Br, P2 = Ai Bi, P3 = (Ar + Ai)(Br + Bi), 9 MFMAs per
+// complex tile-step instead of 12; 4 waves of 64 x 64 (3 x 64 accumulators), 3 staging sets
+using TileH4G = Tile<2, 2, 2, 2, 2, 3, true, true>;
 
 __device__ __forceinline__ uint32_t hi16(float x) { return __float_as_uint(x) & 0xffff0000u; }
 // pack the bf16 held in the high halves of two dwords: lo <- a, hi <- b
@@ -782,6 +802,8 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   using namespace xbf;
   constexpr int BM = TL::BM, BN = TL::BN, BK = TL::BK, WMW = TL::WMW, TI = TL::TI, TJ = TL::TJ;
   constexpr int SUBA = TL::SUBA, SUBB = TL::SUBB, BUF = TL::BUF, NTM = SP::NTERM;
+  constexpr bool G3 = TL::G3;
+  constexpr int NGRP = TL::NGRP, NACC = G3 ? 3 : 2;
   static_assert(TL::NTERM == SP::NTERM, "tile / split terms");
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
 
@@ -842,7 +864,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   // term planes: 0..NTM-1 = re terms (largest first), NTM..2 NTM-1 = im terms
   const int sc = op ? scb : sca;
   const int sub = op ? SUBB : SUBA;
-  const int obase = op ? 2 * NTM * SUBA : 0;
+  const int obase = op ? NGRP * NTM * SUBA : 0;
   const int toff0 = swz(trow, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
   const int toff1 = swz(trow + 1, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
   auto put = [&](const float (&re)[KPT], const float (&im)[KPT], char* base, int toff) {
@@ -853,6 +875,15 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
     SP::template split<KPT>(im, sc, t);
 #pragma unroll
     for (int x = 0; x < NTM; ++x) st_lds<KPT>(base + (NTM + x) * sub + toff, t[x]);
+    if constexpr (G3) {
+      // re + im, scaled one binade lower (|re + im| <= 2 max(|re|, |im|))
+      float sm[KPT];
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) sm[j] = re[j] + im[j];
+      SP::template split<KPT>(sm, sc - 1, t);
+#pragma unroll
+      for (int x = 0; x < NTM; ++x) st_lds<KPT>(base + (2 * NTM + x) * sub + toff, t[x]);
+    }
   };
   auto store_stage = [&](auto set, int buf) {
     constexpr int S = decltype(set)::value;
@@ -866,9 +897,9 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
     put(r1, i1, base, toff1);
   };
 
-  f32x16 acc[2][TI][TJ];
+  f32x16 acc[NACC][TI][TJ];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < NACC; ++x)
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -881,10 +912,10 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
 #pragma unroll
   for (int i = 0; i < TI; ++i) a_off[i] = swz(wm * TL::WM + i * 32 + fr, fh);
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) b_off[j] = 2 * NTM * SUBA + swz(wn * TL::WN + j * 32 + fr, fh);
+  for (int j = 0; j < TJ; ++j) b_off[j] = NGRP * NTM * SUBA + swz(wn * TL::WN + j * 32 + fr, fh);
 
-  typedef uint4 FragA[2 * NTM][TI];
-  typedef uint4 FragB[2 * NTM][TJ];
+  typedef uint4 FragA[NGRP * NTM][TI];
+  typedef uint4 FragB[NGRP * NTM][TJ];
   // planes in the order the MFMA pairs first use them (pair 0's four first), so the first MFMAs
   // of a step wait for a third to a half of the step's fragment reads, not all of them
   auto read_frags = [&](const char* s, FragA& fa, FragB& fb) {
@@ -895,7 +926,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       if (!ra[xa]) {
         ra[xa] = true;
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < NGRP; ++h)
 #pragma unroll
           for (int i = 0; i < TI; ++i)
             fa[h * NTM + xa][i] = *reinterpret_cast<const uint4*>(s + (h * NTM + xa) * SUBA + a_off[i]);
@@ -903,7 +934,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       if (!rb[xb]) {
         rb[xb] = true;
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < NGRP; ++h)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
             fb[h * NTM + xb][j] = *reinterpret_cast<const uint4*>(s + (h * NTM + xb) * SUBB + b_off[j]);
@@ -918,6 +949,16 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       for (int i = 0; i < TI; ++i) {
         const uint4 ar = fa[SP::pa(q)][i];
         const uint4 ai = fa[NTM + SP::pa(q)][i];
+        if constexpr (G3) {
+          const uint4 as = fa[2 * NTM + SP::pa(q)][i];
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[0][i][j] = SP::mfma(ar, fb[SP::pb(q)][j], acc[0][i][j]);
+            acc[1][i][j] = SP::mfma(ai, fb[NTM + SP::pb(q)][j], acc[1][i][j]);
+            acc[2][i][j] = SP::mfma(as, fb[2 * NTM + SP::pb(q)][j], acc[2][i][j]);
+          }
+          continue;
+        }
         const uint4 nai = neg8(ai);
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
@@ -951,9 +992,9 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       // fragment reads first, then every MFMA followed by up to 3 VALU (the split, the sign
       // flips), the split's LDS stores spread evenly: without this the compiler issued the split
       // and the MFMAs largely back to back (the no-MFMA variant's time added to the MFMA time)
-      constexpr int NM = SP::NPAIR * TI * TJ * 4;
-      constexpr int NR = 2 * NTM * (TI + TJ);
-      constexpr int NWR = 2 * 2 * NTM;  // LDS stores per thread: 2 rows x (re, im) x terms
+      constexpr int NM = SP::NPAIR * TI * TJ * (G3 ? 3 : 4);
+      constexpr int NR = NGRP * NTM * (TI + TJ);
+      constexpr int NWR = 2 * NGRP * NTM;  // LDS stores per thread: 2 rows x planes
       __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
       Interleave<0, NM, 3, (NM / NWR > 0 ? NM / NWR : 1)>::run();
     }
@@ -1010,7 +1051,14 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
           const int64_t gm = m0 + wm * TL::WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int64_t gn = n0 + wn * TL::WN + j * 32 + (lane & 31);
           float2* p = reinterpret_cast<float2*>(Cout + (gm * ldo + gn) * 2);
-          float2 v = make_float2(ldexpf(acc[0][i][j][r], unsc), ldexpf(acc[1][i][j][r], unsc));
+          float2 v;
+          if constexpr (G3) {
+            // P3 was accumulated from sums scaled one binade lower on both sides: 4 P3 (exact)
+            const float p1 = acc[0][i][j][r], p2 = acc[1][i][j][r];
+            v = make_float2(ldexpf(p1 - p2, unsc), ldexpf(4.f * acc[2][i][j][r] - p1 - p2, unsc));
+          } else {
+            v = make_float2(ldexpf(acc[0][i][j][r], unsc), ldexpf(acc[1][i][j][r], unsc));
+          }
           if constexpr (decltype(with_beta)::value) {
             const float2 o = *p;
             v.x += beta * o.x;
@@ -1353,10 +1401,13 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.amax_a = amax;
             f.amax_b = amax + 1;
           }
-          static const int var = [] { const char* e = getenv("TQ_GEMM_F16_VAR"); return e ? atoi(e) : 0; }();
+          const int var = gemm_f16_var();
           if (var == 1)
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH4, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH4::NT), 0, stream, f);
+          else if (var == 2)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH4G, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH4G::NT), 0, stream, f);
           else
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH::NT), 0, stream, f);
