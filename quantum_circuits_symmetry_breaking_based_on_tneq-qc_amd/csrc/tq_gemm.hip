@@ -1316,8 +1316,9 @@ int fast_c64_splits_t(int transA, int transB, int64_t M, int64_t N, int64_t K, i
   if (M % TL::BM || N % TL::BN || K % BK || K == 0) return 0;
   const int64_t tiles = (M / TL::BM) * (N / TL::BN) * batch;
   int s = 1;
-  // fill the 256 CUs with one block each; keep >= 32 K-tiles per split
-  while (tiles * s * 2 <= 256 && K % ((int64_t)s * 2 * BK) == 0 && K / ((int64_t)s * 2 * BK) >= 32) s *= 2;
+  // fill the 256 CUs with one block each; keep >= 8 K-tiles per split (C3's boundary GEMM,
+  // 256 x 256 x 512, ran on 4 blocks with the earlier 32)
+  while (tiles * s * 2 <= 256 && K % ((int64_t)s * 2 * BK) == 0 && K / ((int64_t)s * 2 * BK) >= 8) s *= 2;
   if (tiles * s > INT32_MAX) return 0;
   return s;
 }
