@@ -20,6 +20,7 @@ bool gemm_3m();
 bool gemm_bf16();
 bool gemm_f16();
 int gemm_f16_var();
+bool gemm_presplit_enabled();
 bool gemm_configure(const char* key, int64_t v);
 bool graphs_enabled();
 bool sweeps_enabled_global();
@@ -32,6 +33,7 @@ extern "C" int64_t tq_library_query(const char* key) {
   if (k == "gemm_bf16") return tq::gemm_bf16() ? 1 : 0;
   if (k == "gemm_f16") return tq::gemm_f16() ? 1 : 0;
   if (k == "gemm_f16_var") return tq::gemm_f16_var();
+  if (k == "gemm_presplit") return tq::gemm_presplit_enabled() ? 1 : 0;
   if (k == "graphs") return tq::graphs_enabled() ? 1 : 0;
   if (k == "sweep") return tq::sweeps_enabled_global() ? 1 : 0;
 
@@ -220,6 +222,8 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "n_kernels") return (int64_t)P.ops.size();
   if (k == "graph_builds") return P.graph_builds;
   if (k == "graph_launches") return P.graph_launches;
+  if (k == "n_presplit") return P.n_ps;
+  if (k == "presplit_fallbacks") return P.ps_fallbacks;
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;
   if (k == "n_permute") return P.n_permute;

@@ -96,7 +96,26 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
                 const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
                 void* workspace, size_t ws_bytes, hipStream_t stream,
-                const uint32_t* amax_a = nullptr, const uint32_t* amax_b = nullptr);
+                const uint32_t* amax_a = nullptr, const uint32_t* amax_b = nullptr,
+                const struct GemmPresplit* presplit = nullptr);
+// Operands stored as f16 terms by their producers (S2Op::split_sc; complex64 K-outer f16 path):
+// every element holds (h_re, h_im | l_re, l_im) of the value scaled by 2^sc.  The GEMM checks the
+// producers' true max words against the scales: outside the window (max * 2^sc in [2^0, 2^15))
+// it writes zeros and sets *bad = 1 (else 0), and the plan re-runs that slice on the split path.
+struct GemmPresplit {
+  const int32_t* sc_a = nullptr;
+  const int32_t* sc_b = nullptr;
+  uint32_t* bad = nullptr;
+};
+// plan-time / run-time eligibility of a GEMM for pre-split operands (the launch would take the
+// f16 split kernel), the library switch (TQ_GEMM_PRESPLIT, "gemm_presplit") and the scale
+// prediction offset (testing: "presplit_bias" forces the fallback)
+bool gemm_c64_presplit_ok(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
+                          int64_t lda, int64_t ldb);
+bool gemm_presplit_enabled();
+// per slice, before the producers: sc[i] = scale for the next operand from the previous max
+// (amax[i]; 0 = none yet), amax[i] = 0
+int presplit_prep_launch(uint32_t* amax, int32_t* sc, int n, hipStream_t stream);
 // amax_a / amax_b (optional, complex64): float bits of max |re|, |im| over A / B, written by the
 // operands' producers (plan: the sweep ops that store them); the f16-split kernel then skips its
 // own max pre-pass over A and B

@@ -53,8 +53,25 @@ bool gemm_bf16() { return g_gemm_bf16.load(std::memory_order_relaxed) != 0; }
 bool gemm_f16() { return g_gemm_f16.load(std::memory_order_relaxed) != 0; }
 // runtime switch (tq_library_set): affects launches issued after the call (plans replaying a
 // captured hipGraph keep the kernels they captured)
+// pre-split operands (GemmPresplit) are opt-in: measured on C4 (r02) the GEMM
+// took 1.375 ms vs 1.34-1.39 ms on the split path while the producers' f16 stores added 0.37 ms
+// of sweep time per step -- the split arithmetic is not what bounds the kernel
+static int env_on(const char* name) {
+  const char* e = getenv(name);
+  return (e && e[0] == '1') ? 1 : 0;
+}
+static std::atomic<int> g_gemm_presplit{env_on("TQ_GEMM_PRESPLIT")};
+static std::atomic<int> g_presplit_bias{env_int("TQ_PRESPLIT_BIAS")};
+bool gemm_presplit_enabled() { return g_gemm_presplit.load(std::memory_order_relaxed) != 0; }
+int presplit_bias() { return g_presplit_bias.load(std::memory_order_relaxed); }
 bool gemm_configure(const char* key, int64_t v) {
   const std::string k(key);
+  if (k == "gemm_presplit") { g_gemm_presplit = v ? 1 : 0; return true; }
+  if (k == "presplit_bias") {
+    if (v < -64 || v > 64) return false;
+    g_presplit_bias = (int)v;
+    return true;
+  }
   if (k == "gemm_3m") { g_gemm_3m = v ? 1 : 0; return true; }
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
@@ -403,6 +420,9 @@ struct FastArgs {
   float beta;
   const uint32_t* amax_a;  // f16 split kernel: max |x| bits of A / B (producer or absmax pre-pass)
   const uint32_t* amax_b;
+  const int32_t* sc_a;     // pre-split operands (SplitPre): the producers' scales, window flag
+  const int32_t* sc_b;
+  uint32_t* bad;
 };
 
 template <int N>
@@ -660,7 +680,7 @@ __device__ __forceinline__ uint32_t pk(uint32_t a, uint32_t b) { return __builti
 // Term pairs kept (A term, B term), smallest first: mh hm lh hl hh... the six down to 2^-16.
 struct SplitBF16 {
   static constexpr int NTERM = 3, NPAIR = 6;
-  static constexpr bool SCALED = false;
+  static constexpr bool SCALED = false, PRE = false;
   static constexpr int pa(int q) { return q == 0 ? 1 : q == 2 ? 2 : q == 4 ? 1 : 0; }  // 1 0 2 0 1 0
   static constexpr int pb(int q) { return q == 0 ? 1 : q == 1 ? 2 : q == 3 ? 1 : 0; }  // 1 2 0 1 0 0
   template <int N>
@@ -692,7 +712,7 @@ struct SplitBF16 {
 // the operand's max.  Pairs kept: lh, hl, hh; the dropped ll is <= 2^-24 relative.
 struct SplitF16 {
   static constexpr int NTERM = 2, NPAIR = 3;
-  static constexpr bool SCALED = true;
+  static constexpr bool SCALED = true, PRE = false;
   static constexpr int pa(int q) { return q == 0 ? 1 : 0; }  // 1 0 0
   static constexpr int pb(int q) { return q == 1 ? 1 : 0; }  // 0 1 0
   // per pair of values: 2 v_ldexp_f32, v_cvt_pk_f16_f32 (h), 2 v_fma_mix_f32 (r = x - h, reading
@@ -717,6 +737,13 @@ struct SplitF16 {
   }
 };
 
+// f16 terms split by the operand's producer (S2Op::split_sc): every complex64 element holds
+// (h_re, h_im | l_re, l_im) as four f16 of the value scaled by 2^sc; the GEMM only regroups the
+// halves into its term planes (v_perm_b32, 2 per 4 k of a row and plane)
+struct SplitPre : SplitF16 {
+  static constexpr bool PRE = true;
+};
+
 // scheduling pattern (sched_group_barrier, one scheduling region): MFMA i, then up to V VALU,
 // and one LDS store after every E-th MFMA
 template <int I, int NM, int V, int E> struct Interleave {
@@ -737,6 +764,31 @@ __device__ __forceinline__ int scale_exp(uint32_t bits) {
   if (bits == 0 || E == 255) return 0;
   const int e = E ? E - 127 : (31 - __clz((int)(bits & 0x7fffff))) - 149;
   return 14 - e;
+}
+
+// pre-split operands: floor(log2 max) + sc in [0, 14] (max == 0: every term is zero, valid)
+__device__ __forceinline__ bool presplit_in_window(uint32_t bits, int sc) {
+  const int E = (int)((bits >> 23) & 0xff);
+  if (bits == 0) return true;
+  if (E == 255) return false;
+  const int e = E ? E - 127 : (31 - __clz((int)(bits & 0x7fffff))) - 149;
+  return e + sc >= 0 && e + sc <= 14;
+}
+
+// scale of the next slice's operand from this slice's max: max * 2^sc near 2^7 (7 binades of
+// headroom either way); no max yet: sc = 10 (|x| ~ 1e-3 .. 16)
+__global__ void presplit_prep_kernel(uint32_t* amax, int32_t* sc, int n, int bias) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t bits = amax[i];
+    const int E = (int)((bits >> 23) & 0xff);
+    int s = 10;
+    if (bits != 0 && E != 255) {
+      const int e = E ? E - 127 : (31 - __clz((int)(bits & 0x7fffff))) - 149;
+      s = 7 - e;
+    }
+    sc[i] = s + bias;
+    amax[i] = 0;
+  }
 }
 
 template <int N>
@@ -829,7 +881,26 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   const float2* B = reinterpret_cast<const float2*>(g.B) + ((int64_t)b * g.sB + kbeg * g.ldb + n0);
   // power-of-two operand scales (f16 terms): from the operands' max |x| (absmax_kouter_kernel)
   int sca = 0, scb = 0;
-  if constexpr (SP::SCALED) {
+  if constexpr (SP::PRE) {
+    // the producers scaled by sc_a / sc_b (predicted from the previous slice): valid while the
+    // true max lands in [2^0, 2^15) -- no f16 overflow, rounding <= 2^-25 of the max; otherwise
+    // this launch writes zeros and flags the slice for the split path
+    sca = *g.sc_a;
+    scb = *g.sc_b;
+    const bool ok = presplit_in_window(*g.amax_a, sca) && presplit_in_window(*g.amax_b, scb);
+    if (L == 0 && tid == 0) *g.bad = ok ? 0u : 1u;
+    if (!ok) {
+      const bool part = g.splits > 1;
+      float* Co = part ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * 2 : g.C + (int64_t)b * g.sC * 2;
+      const int64_t ldz = part ? g.N : g.ldc;
+      for (int e = tid; e < BM * BN; e += TL::NT) {
+        const int64_t gm = m0 + e / BN, gn = n0 + e % BN;
+        float2* p = reinterpret_cast<float2*>(Co + (gm * ldz + gn) * 2);
+        *p = (part || g.beta == 0.f) ? make_float2(0.f, 0.f) : make_float2(p->x * g.beta, p->y * g.beta);
+      }
+      return;
+    }
+  } else if constexpr (SP::SCALED) {
     sca = scale_exp(*g.amax_a);
     scb = scale_exp(*g.amax_b);
   }
@@ -868,6 +939,23 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   const int toff0 = swz(trow, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
   const int toff1 = swz(trow + 1, (tkg * KPT) >> 3) + ((tkg * KPT) & 7) * 2;
   auto put = [&](const float (&re)[KPT], const float (&im)[KPT], char* base, int toff) {
+    if constexpr (SP::PRE) {
+      // re[j] = bits of (h_re, h_im), im[j] = bits of (l_re, l_im) of k = j: planes h_re, l_re,
+      // h_im, l_im from the low / high halves
+      uint32_t q[4][KPT / 2];
+#pragma unroll
+      for (int j = 0; j < KPT / 2; ++j) {
+        const uint32_t a0 = __float_as_uint(re[2 * j]), a1 = __float_as_uint(re[2 * j + 1]);
+        const uint32_t b0 = __float_as_uint(im[2 * j]), b1 = __float_as_uint(im[2 * j + 1]);
+        q[0][j] = __builtin_amdgcn_perm(a1, a0, 0x05040100u);
+        q[1][j] = __builtin_amdgcn_perm(b1, b0, 0x05040100u);
+        q[2][j] = __builtin_amdgcn_perm(a1, a0, 0x07060302u);
+        q[3][j] = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) st_lds<KPT>(base + x * sub + toff, q[x]);
+      return;
+    }
     uint32_t t[NTM][KPT / 2];
     SP::template split<KPT>(re, sc, t);
 #pragma unroll
@@ -1328,6 +1416,24 @@ int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int
   return fast_c64_splits_t<fastc64::Tile3M>(transA, transB, M, N, K, batch);
 }
 
+}  // namespace
+
+bool gemm_c64_presplit_ok(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
+                          int64_t lda, int64_t ldb) {
+  return gemm_presplit_enabled() && gemm_bf16() && gemm_f16() && gemm_f16_var() == 0 && !fast_disabled() &&
+         batch == 1 && lda % 2 == 0 && ldb % 2 == 0 && lda < (int64_t(1) << 24) && ldb < (int64_t(1) << 24) &&
+         fast_c64_splits_t<xbf::TileX>(transA, transB, M, N, K, batch) > 0;
+}
+
+int presplit_prep_launch(uint32_t* amax, int32_t* sc, int n, hipStream_t stream) {
+  if (n <= 0) return TQ_OK;
+  hipLaunchKernelGGL(xbf::presplit_prep_kernel, dim3(1), dim3(64), 0, stream, amax, sc, n, presplit_bias());
+  TQ_HIP(hipGetLastError());
+  return TQ_OK;
+}
+
+namespace {
+
 // C_b = sum_s W[s][b] + beta * C_b
 template <typename R>
 __global__ void __launch_bounds__(kThreads)
@@ -1360,7 +1466,8 @@ template <typename R, bool CPLX>
 int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
                  const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB,
                  double beta, void* C, int64_t ldc, int64_t sC, void* W, size_t wsb,
-                 hipStream_t stream, const uint32_t* amax_a, const uint32_t* amax_b) {
+                 hipStream_t stream, const uint32_t* amax_a, const uint32_t* amax_b,
+                 const GemmPresplit* ps) {
   using C_ = Cfg<R, CPLX>;
   constexpr int EW = CPLX ? 2 : 1;
   constexpr int VE = 16 / (EW * (int)sizeof(R));
@@ -1370,6 +1477,11 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
                     ldb % 2 == 0 && (batch == 1 || (sA % 2 == 0 && sB % 2 == 0)) &&
                     lda < (int64_t(1) << 24) && ldb < (int64_t(1) << 24);
     const size_t need = (size_t)fs * batch * M * N * 8;
+    if (ps && !(fs > 0 && al && (fs == 1 || (W != nullptr && wsb >= need)) && !fast_disabled() &&
+                gemm_bf16() && gemm_f16())) {
+      set_error("gemm: pre-split operands but the f16 split path is not available");
+      return TQ_ERR_INVALID;
+    }
     if (fs > 0 && al && (fs == 1 || (W != nullptr && wsb >= need)) && !fast_disabled()) {
       FastArgs f{};
       f.A = (const float*)A; f.B = (const float*)B; f.C = (float*)C; f.W = (float*)W;
@@ -1403,7 +1515,13 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.amax_b = amax + 1;
           }
           const int var = gemm_f16_var();
-          if (var == 1)
+          if (ps) {
+            f.sc_a = ps->sc_a;
+            f.sc_b = ps->sc_b;
+            f.bad = ps->bad;
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitPre>), dim3((unsigned)nb),
+                               dim3(xbf::TileH::NT), 0, stream, f);
+          } else if (var == 1)
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH4, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH4::NT), 0, stream, f);
           else if (var == 2)
@@ -1565,8 +1683,12 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
                 const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
                 void* workspace, size_t ws_bytes, hipStream_t stream, const uint32_t* amax_a,
-                const uint32_t* amax_b) {
+                const uint32_t* amax_b, const GemmPresplit* presplit) {
   TQ_CHECK_ARG(dtype_valid(dtype), "dtype");
+  TQ_CHECK_ARG(presplit == nullptr || (dtype == TQ_C64 && amax_a && amax_b && presplit->sc_a &&
+                                       presplit->sc_b && presplit->bad &&
+                                       gemm_c64_presplit_ok(transA, transB, M, N, K, batch, lda, ldb)),
+               "pre-split operands need the complex64 f16 split path");
   TQ_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && batch >= 0, "negative size");
   TQ_CHECK_ARG(transA == 0 || transA == 1, "transA");
   TQ_CHECK_ARG(transB == 0 || transB == 1, "transB");
@@ -1577,16 +1699,16 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
   switch (dtype) {
     case TQ_F32:
       return launch_typed<float, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
     case TQ_C64:
       return launch_typed<float, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
+                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
     case TQ_F64:
       return launch_typed<double, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
+                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
     case TQ_C128:
       return launch_typed<double, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b);
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
   }
   return TQ_ERR_INVALID;
 }

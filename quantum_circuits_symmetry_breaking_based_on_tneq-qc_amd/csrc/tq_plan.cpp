@@ -259,6 +259,10 @@ class Compiler {
     }
     P_.amax_off = tb;
     tb += ((size_t)(P_.n_amax_once + P_.n_amax_slice) * sizeof(uint32_t) + kAlign - 1) / kAlign * kAlign;
+    P_.sc_off = tb;
+    tb += ((size_t)P_.n_amax_slice * sizeof(int32_t) + kAlign - 1) / kAlign * kAlign;
+    P_.bad_off = tb;
+    if (P_.n_ps) tb += ((size_t)P_.n_slices * sizeof(uint32_t) + kAlign - 1) / kAlign * kAlign;
     P_.table_bytes = tb;
     for (auto& op : P_.ops) {
       (op.invariant ? P_.flops_once : P_.flops_slice) += op.flops;
@@ -345,6 +349,40 @@ class Compiler {
       P_.ops[i].amax_a = P_.ops[prod_a[i]].amax_word;
       P_.ops[i].amax_b = P_.ops[prod_b[i]].amax_word;
       P_.ops[i].note += " amax<-op" + std::to_string(prod_a[i]) + ",op" + std::to_string(prod_b[i]);
+    }
+    // pre-split candidates: per-slice GEMM, per-slice producers that store nothing else read
+    // (scan forward from the producer until its bytes are overwritten), batch 1, no beta
+    P_.n_ps = 0;
+    auto exclusive = [&](int j, int gi) {
+      int sp, spo;
+      int64_t lo, hi, olo, ohi;
+      const Op& w = P_.ops[j];
+      if (!span(w.c, w.nc, &sp, &lo, &hi)) return false;
+      auto hits = [&](const BufRef& r, int64_t n) {
+        return span(r, n, &spo, &olo, &ohi) && spo == sp && olo < hi && lo < ohi;
+      };
+      for (size_t k = j + 1; k < P_.ops.size(); ++k) {
+        const Op& o = P_.ops[k];
+        if ((int)k != gi) {
+          if (hits(o.a, o.na) || hits(o.b, o.nb) || (o.kind == OP_AXPY && hits(o.c, o.nc))) return false;
+          for (auto& g : o.sgates) if (hits(g.g, std::max<int64_t>(g.n, 1))) return false;
+        }
+        if (hits(o.c, o.nc) || (o.nws && hits(o.ws, o.nws))) break;
+      }
+      return true;
+    };
+    const int64_t max_slices = 1 << 16;
+    for (size_t i = 0; i < P_.ops.size(); ++i) {
+      Op& g = P_.ops[i];
+      const int pa = prod_a[i], pb = prod_b[i];
+      if (pa < 0 || pa == pb || g.invariant || g.batch != 1 || P_.n_slices > max_slices) continue;
+      if (P_.ops[pa].invariant || P_.ops[pb].invariant) continue;
+      if (P_.ops[pa].ps_gemm >= 0 || P_.ops[pb].ps_gemm >= 0) continue;
+      if (!exclusive(pa, (int)i) || !exclusive(pb, (int)i)) continue;
+      g.ps_cand = true;
+      P_.ops[pa].ps_gemm = P_.ops[pb].ps_gemm = (int)i;
+      g.note += " presplit";
+      ++P_.n_ps;
     }
   }
 
@@ -839,6 +877,13 @@ class Compiler {
     }();
     return v != 0;
   }
+  static bool s2_epi_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_EPI");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
   static bool s2_enabled() {
     static const int v = [] {
       const char* e = getenv("TQ_SWEEP2");
@@ -912,6 +957,8 @@ class Compiler {
     S2Desc d;
     d.ngates = (int)c.gates.size();
     std::vector<std::vector<int>> kdep(c.gates.size()), ndep(c.gates.size());
+    std::vector<int> last_np;   // output positions of the last gate, index bit order
+    int last_nk = 0;            // its input index bits (they are the first output bits)
     for (size_t j = 0; j < c.gates.size(); ++j) {
       const auto& g = c.gates[j];
       std::vector<MB> kb, nb;   // index bits, least significant first
@@ -950,6 +997,7 @@ class Compiler {
         np.push_back(p);
         used = std::max(used, p + 1);
       }
+      if (j + 1 == c.gates.size()) { last_np = np; last_nk = (int)kp.size(); }
       for (int k = 0; k < G.K; ++k) {
         int v = 0;
         for (size_t t = 0; t < kp.size(); ++t) if ((k >> t) & 1) v |= 1 << kp[t];
@@ -1005,6 +1053,77 @@ class Compiler {
     auto by_w = [](const CBit& a, const CBit& b) { return a.w < b.w; };
     std::sort(ld.begin(), ld.end(), by_w);
     std::sort(st.begin(), st.end(), by_w);
+    // Store-phase epilogue: the last gate (K <= N, its inputs on the first output positions) is
+    // applied in registers while the tile leaves LDS -- one LDS write + read of the largest
+    // working set and one barrier less per chunk.  Its output position bits move to the lowest
+    // register-slot bits of the store enumeration (the lane bits keep the smallest strides);
+    // the positions it adds are not live before it, so input k sits in slot r0 + k.
+    // register blocks of consecutive square gates (S2Desc::pmeta): the pass starting at gate j
+    // ends before block_span(j, ng); bm = its block positions, live = the live positions
+    const int B = s2_block_bits((int)P_.esz, int64_t(1) << (lc + used));
+    auto kmask_of = [&](int j) {
+      uint32_t m = 0;
+      for (int k = 0; k < d.gate[j].K; ++k) m |= (uint32_t)kdep[j][k];
+      return m;
+    };
+    auto square = [&](int j) {
+      const S2Gate& G = d.gate[j];
+      if (G.K != G.N || (G.K != 2 && G.K != 4)) return false;
+      for (int k = 0; k < G.K; ++k) if (kdep[j][k] != ndep[j][k]) return false;
+      return true;
+    };
+    const bool blocks = s2_blocks_enabled();
+    auto block_span = [&](int j, int ng, uint32_t* bm_out, uint32_t* live_out) {
+      int e = j + 1;
+      uint32_t bm = 0, live = 0;
+      if (blocks && square(j)) {
+        bm = kmask_of(j);
+        live = d.gate[j].pass_mask | bm;
+        while (e < ng && e - j < kS2BlkMaxGates && square(e) &&
+               __builtin_popcount(bm | kmask_of(e)) <= B)
+          bm |= kmask_of(e), ++e;
+      }
+      if (e - j >= 2) {
+        // pad the block with untouched live positions up to B bits (fewer, larger groups)
+        for (int q = 0; q < kS2MaxPos && __builtin_popcount(bm) < B; ++q)
+          if (((live >> q) & 1) && !((bm >> q) & 1)) bm |= 1u << q;
+        if (__builtin_popcount(bm) != B) e = j + 1;
+      }
+      *bm_out = bm;
+      *live_out = live;
+      return e;
+    };
+    // a last gate inside a register block costs no pass of its own: no epilogue then
+    bool last_alone = true;
+    {
+      const int ng = (int)c.gates.size();
+      uint32_t bm, lv;
+      for (int j = 0; j < ng;) {
+        const int e = block_span(j, ng, &bm, &lv);
+        if (e == ng) last_alone = e - j == 1;
+        j = e;
+      }
+    }
+    d.epi = 0;
+    if (s2_epi_enabled() && last_alone && !last_np.empty()) {
+      const S2Gate& G = d.gate[c.gates.size() - 1];
+      const int nn = (int)last_np.size();
+      bool ok = G.K <= G.N && G.K * G.N <= 16 && G.N >= 2 && last_nk <= nn &&
+                (int)st.size() >= kS2LogThreads + nn && (int)st.size() <= kS2LogThreads + 4;
+      std::vector<CBit> rest, moved(nn);
+      for (size_t t = 0; ok && t < st.size(); ++t) {
+        const auto it = std::find(last_np.begin(), last_np.end(), st[t].pos);
+        if (st[t].col >= 0 || it == last_np.end()) { rest.push_back(st[t]); continue; }
+        if (t < 5) ok = false;   // keep the coalesced 32-lane runs
+        moved[it - last_np.begin()] = st[t];
+      }
+      if (ok) {
+        st.assign(rest.begin(), rest.begin() + kS2LogThreads);
+        st.insert(st.end(), moved.begin(), moved.end());
+        st.insert(st.end(), rest.begin() + kS2LogThreads, rest.end());
+        d.epi = (int)c.gates.size();
+      }
+    }
     // swizzle vectors: the first 4 / 5 chunk bits of each enumeration (one 16- / 32-lane group)
     // must map to independent bank slots (mod 16 / mod 32)
     int vsw[kS2MaxPos];
@@ -1104,19 +1223,7 @@ class Compiler {
     }
     // passes: register blocks of consecutive square gates (S2Desc::pmeta), single gates otherwise
     {
-      const int ng = (int)c.gates.size();
-      const int B = s2_block_bits((int)P_.esz, int64_t(1) << (d.logC + used));
-      auto kmask_of = [&](int j) {
-        uint32_t m = 0;
-        for (int k = 0; k < d.gate[j].K; ++k) m |= (uint32_t)kdep[j][k];
-        return m;
-      };
-      auto square = [&](int j) {
-        const S2Gate& G = d.gate[j];
-        if (G.K != G.N || (G.K != 2 && G.K != 4)) return false;
-        for (int k = 0; k < G.K; ++k) if (kdep[j][k] != ndep[j][k]) return false;
-        return true;
-      };
+      const int ng = (int)c.gates.size() - (d.epi ? 1 : 0);   // the epilogue gate is no pass
       auto group_lut = [&](uint32_t pass_mask, int32_t* lut) {
         for (int jj = 0; jj < 64; ++jj) {
           const int half = jj >> 5, v = jj & 31;
@@ -1131,27 +1238,13 @@ class Compiler {
           lut[jj] = (base << d.logC) ^ (sw & cmask);
         }
       };
-      const bool blocks = s2_blocks_enabled();
       int j = 0;
       d.npass = 0;
       while (j < ng) {
         int32_t* pm = d.pmeta[d.npass++];
         pm[kS2PmFirst] = j;
-        int e = j + 1;
         uint32_t bm = 0, live = 0;
-        if (blocks && square(j)) {
-          bm = kmask_of(j);
-          live = d.gate[j].pass_mask | bm;
-          while (e < ng && e - j < kS2BlkMaxGates && square(e) &&
-                 __builtin_popcount(bm | kmask_of(e)) <= B)
-            bm |= kmask_of(e), ++e;
-        }
-        if (e - j >= 2) {
-          // pad the block with untouched live positions up to B bits (fewer, larger groups)
-          for (int q = 0; q < kS2MaxPos && __builtin_popcount(bm) < B; ++q)
-            if (((live >> q) & 1) && !((bm >> q) & 1)) bm |= 1u << q;
-          if (__builtin_popcount(bm) != B) e = j + 1;
-        }
+        const int e = block_span(j, ng, &bm, &live);
         if (e - j < 2) {
           pm[kS2PmCount] = 1;
           pm[kS2PmB] = 0;
@@ -1183,7 +1276,7 @@ class Compiler {
       }
     }
     if (getenv("TQ_DEBUG_S2")) {
-      fprintf(stderr, "S2 cols=2^%d logC=%d used=%d ld:", d.colbits, d.logC, used);
+      fprintf(stderr, "S2 cols=2^%d logC=%d used=%d epi=%d ld:", d.colbits, d.logC, used, d.epi);
       for (int t = 0; t < d.nld; ++t) fprintf(stderr, " %lld/%x", (long long)d.ld_w[t], d.ld_code[t]);
       fprintf(stderr, " | st:");
       for (int t = 0; t < d.nst; ++t) fprintf(stderr, " %lld/%x", (long long)d.st_w[t], d.st_code[t]);
@@ -1191,7 +1284,12 @@ class Compiler {
       for (int p = 0; p < kS2MaxPos; ++p) fprintf(stderr, " %d", d.vsw[p]);
       fprintf(stderr, " | gates:");
       for (size_t j = 0; j < c.gates.size(); ++j)
-        fprintf(stderr, " [K%d N%d pass%x]", d.gate[j].K, d.gate[j].N, d.gate[j].pass_mask);
+      {
+        uint32_t km = 0, nm = 0;
+        for (int k = 0; k < d.gate[j].K; ++k) km |= (uint32_t)kdep[j][k];
+        for (int n = 0; n < d.gate[j].N; ++n) nm |= (uint32_t)ndep[j][n];
+        fprintf(stderr, " [K%d N%d pass%x in%x out%x]", d.gate[j].K, d.gate[j].N, d.gate[j].pass_mask, km, nm);
+      }
       fprintf(stderr, "\n");
     }
     *out = d;
@@ -1272,6 +1370,7 @@ class Compiler {
         << " chunks=" << d.nchunks << (direct ? " ->OUT" : "") << " KxN=";
       for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
       o << " passes=" << d.npass;
+      if (d.epi) o << " epi";
       op.note = o.str();
       P_.ops.push_back(op);
       res.modes = c.out_modes;
@@ -1611,6 +1710,7 @@ int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
     TQ_HIP(hipMemcpyAsync(P.d_tables, host.data(), P.table_bytes, hipMemcpyHostToDevice, stream));
     TQ_HIP(hipStreamSynchronize(stream));
   }
+  if (P.n_ps && !P.h_bad) TQ_HIP(hipHostMalloc((void**)&P.h_bad, P.n_slices * sizeof(uint32_t), hipHostMallocDefault));
   return TQ_OK;
 }
 
@@ -1678,11 +1778,15 @@ void plan_release(Plan& P) {
     if (P.d_tables) (void)hipFree(P.d_tables);
   }
   P.d_arena = P.d_tables = nullptr;
+  if (P.h_bad) (void)hipHostFree(P.h_bad);
+  P.h_bad = nullptr;
 }
 
 
 int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
                  int64_t s_step, int accumulate, hipStream_t stream);
+int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
+                int64_t s_step, int accumulate, hipStream_t stream);
 
 int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
              int64_t s_step, int accumulate, hipStream_t stream) {
@@ -1698,11 +1802,43 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
                  "plan was materialized on device " + std::to_string(P.device) +
                      " but device " + std::to_string(cur) + " is current");
   }
+  // pre-split GEMM operands (Op::ps_cand) when every candidate still takes the f16 split path
+  // under the current library switches, and the stream is not being captured by the caller
+  // (the window check below synchronizes)
+  P.run_mode = 0;
+  if (P.n_ps && P.h_bad) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    TQ_HIP(hipStreamIsCapturing(stream, &cs));
+    bool ok = cs == hipStreamCaptureStatusNone;
+    for (const Op& op : P.ops)
+      if (op.ps_cand && !gemm_c64_presplit_ok(op.transA, op.transB, op.M, op.N, op.K, op.batch, op.lda, op.ldb))
+        ok = false;
+    P.run_mode = ok ? 1 : 0;
+  }
+  TQ_TRY(plan_launch(P, inputs, out, s_begin, s_end, s_step, accumulate, stream));
+  if (P.run_mode) {
+    // slices whose operand max left its scale window produced zeros: add them on the split path
+    const uint32_t* dbad = reinterpret_cast<const uint32_t*>((const char*)P.d_tables + P.bad_off);
+    TQ_HIP(hipMemcpyAsync(P.h_bad, dbad, P.n_slices * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    TQ_HIP(hipStreamSynchronize(stream));
+    std::vector<int64_t> redo;
+    for (int64_t sl = s_begin; sl < s_end; sl += s_step)
+      if (P.h_bad[sl]) redo.push_back(sl);
+    P.run_mode = 0;
+    for (int64_t sl : redo) TQ_TRY(plan_enqueue(P, inputs, out, sl, sl + 1, 1, 1, stream));
+    P.ps_fallbacks += (int64_t)redo.size();
+  }
+  return TQ_OK;
+}
+
+int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
+                int64_t s_step, int accumulate, hipStream_t stream) {
   if (P.profile || !P.use_graph || graphs_disabled())
     return plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, stream);
   Plan::GraphKey key;
   key.inputs.assign(inputs, inputs + P.n_inputs);
   key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
+  key.mode = P.run_mode;
   constexpr size_t kMaxGraphs = 8;
   Plan::GraphEntry* hit = nullptr;
   for (auto& g : P.graphs) if (g.key == key) hit = &g;
@@ -1770,6 +1906,9 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     };
     const double beta_out = first ? 0.0 : 1.0;
     auto amax_word = [&](int w) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.amax_off) + w; };
+    // scale word of per-slice max word w; window flag of slice q
+    auto sc_word = [&](int w) { return reinterpret_cast<int32_t*>((char*)P.d_tables + P.sc_off) + (w - P.n_amax_once); };
+    auto bad_word = [&](int64_t q) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.bad_off) + q; };
     auto launch_one = [&](const Op& op, hipStream_t st) -> int {
       const double beta = op.writes_output ? beta_out : 0.0;
       switch (op.kind) {
@@ -1777,13 +1916,21 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm],
                                   ptr(op.a), ptr(op.c), beta, st));
           break;
-        case OP_GEMM:
+        case OP_GEMM: {
+          GemmPresplit ps;
+          const bool pre = P.run_mode && op.ps_cand;
+          if (pre) {
+            ps.sc_a = sc_word(op.amax_a);
+            ps.sc_b = sc_word(op.amax_b);
+            ps.bad = bad_word(sl);
+          }
           TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
                              op.lda, op.sA, ptr(op.b), op.ldb, op.sB, beta, ptr(op.c), op.ldc, op.sC,
                              op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, st,
                              op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
-                             op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr));
+                             op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, pre ? &ps : nullptr));
           break;
+        }
         case OP_APPLY:
           TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.M, op.K2, op.I, op.N, ptr(op.a), ptr(op.b),
                               op.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[op.gtab]) : nullptr,
@@ -1895,6 +2042,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           o.beta = op.writes_output ? beta_out : 0.0;
           o.use_beta = o.beta != 0.0;
           o.amax = op.amax_word >= 0 ? amax_word(op.amax_word) : nullptr;
+          o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
         }
         TQ_TRY(sweep2_launch(P.dtype, L, stream));
       } else {
@@ -1910,7 +2058,9 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
       for (auto& grp : P.sched_once) TQ_TRY(launch(grp));
     }
-    if (P.n_amax_slice)
+    if (P.n_amax_slice && P.run_mode)   // scales from the previous slice's max, then max = 0
+      TQ_TRY(presplit_prep_launch(amax_word(P.n_amax_once), sc_word(P.n_amax_once), P.n_amax_slice, stream));
+    else if (P.n_amax_slice)
       TQ_HIP(hipMemsetAsync(amax_word(P.n_amax_once), 0, P.n_amax_slice * sizeof(uint32_t), stream));
     for (auto& grp : P.sched_slice) TQ_TRY(launch(grp));
     first = false;

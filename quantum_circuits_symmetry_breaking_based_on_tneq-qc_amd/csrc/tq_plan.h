@@ -67,6 +67,11 @@ struct Op {
   // operand-max words (complex64 f16-split GEMM): a sweep2 op that produces a GEMM operand
   // max-es its stored values into word amax_word; the GEMM reads words amax_a / amax_b
   int amax_word = -1, amax_a = -1, amax_b = -1;
+  // pre-split operands (GemmPresplit): a per-slice GEMM whose two operands are each stored in
+  // full by one per-slice sweep2 op and read by nothing else may take them as f16 terms
+  // (ps_cand); its producers (ps_gemm = that GEMM) then store the terms (S2Op::split_sc)
+  bool ps_cand = false;
+  int ps_gemm = -1;
   // element counts of a / b / c / ws (hazard analysis of the launch schedule)
   int64_t na = 0, nb = 0, nc = 0, nws = 0;
   // bookkeeping
@@ -105,6 +110,13 @@ struct Plan {
   // by slice-invariant producers; per slice: the next n_amax_slice)
   size_t amax_off = 0;
   int n_amax_once = 0, n_amax_slice = 0;
+  // pre-split GEMMs: scale words (one per per-slice max word), one window flag per slice, and
+  // the host copy of the flags (read after an execute call that ran pre-split GEMMs)
+  size_t sc_off = 0, bad_off = 0;
+  int n_ps = 0;               // pre-split candidate GEMMs
+  uint32_t* h_bad = nullptr;  // pinned, n_slices words
+  int run_mode = 0;           // 1: this execute call runs the candidates pre-split
+  int64_t ps_fallbacks = 0;   // slices re-run on the split path (operand max left the window)
   size_t arena_bytes = 0;
   size_t pinned_base = 0;             // pinned (hoisted, slice-invariant) results live above this
   void* d_arena = nullptr;
@@ -131,8 +143,10 @@ struct Plan {
     void* out = nullptr;
     int64_t b = 0, e = 0, s = 0;
     int acc = 0;
+    int mode = 0;   // Plan::run_mode the graph was captured with
     bool operator==(const GraphKey& o) const {
-      return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc;
+      return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc &&
+             mode == o.mode;
     }
   };
   bool use_graph = true;

@@ -43,7 +43,11 @@ struct S2Desc {
   int64_t ncols = 0, nchunks = 0;
   int logC = 0, colbits = 0;     // columns per chunk (log2), column index bits
   int nld = 0, nst = 0;          // chunk bits of the load (X) / store (Y) enumerations
-  int ngates = 0, pad = 0;
+  int ngates = 0;
+  // 1 + index of the last gate when the store phase applies it in registers (0: every gate is a
+  // pass): its output index bits are the lowest register-slot bits of the store enumeration, so
+  // a thread's slots r0 .. r0+N-1 hold one group's outputs and r0 .. r0+K-1 its inputs
+  int epi = 0;
   int64_t ld_w[16] = {}, st_w[16] = {};      // memory weight of each chunk bit (ascending)
   int32_t ld_code[16] = {}, st_code[16] = {};
   // LDS element address of each chunk bit: every LDS address is an XOR of these
@@ -96,6 +100,10 @@ struct S2Op {
   // complex64 only, optional: the op atomically max-es the float bits of max |re|, |im| over
   // every value it stores into *amax (zeroed before; the max a consuming f16-split GEMM scales by)
   uint32_t* amax = nullptr;
+  // complex64 only, optional: store every value as the f16 terms of v * 2^sc, sc = *split_sc
+  // ((h_re, h_im | l_re, l_im) in the element's 8 bytes; the consuming GEMM's SplitPre); amax
+  // still tracks the unscaled values
+  const int32_t* split_sc = nullptr;
 };
 
 struct S2Launch {

@@ -58,6 +58,13 @@ struct S2Hot {
 static_assert(kGmNaddr + kS2MaxKN <= kGm, "gate meta layout");
 static_assert(kLut == 64, "lut layout shared with S2Desc::lut");
 
+#if defined(TQ_S2_DIAG) && TQ_S2_DIAG == 2
+// development diagnostic: no HBM stores (a runtime condition that never holds keeps the work)
+#define TQ_ST(p, v) do { if (use_beta == 12345) *(p) = (v); } while (0)
+#else
+#define TQ_ST(p, v) (*(p) = (v))
+#endif
+
 #ifdef TQ_S2_TIMING
 // development instrumentation (built only with -DTQ_S2_TIMING): workgroup 0 of every op records
 // wall-clock stamps (100 MHz) at its phase boundaries
@@ -78,6 +85,21 @@ __device__ __forceinline__ T scale_add(T v, T y, double beta) {
 }
 
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// f16 terms of v * 2^sc (S2Op::split_sc; the consuming GEMM's xbf::SplitPre): h = f16(xs) (round
+// to nearest), l = f16(xs - h) (xs - h exact in f32, read from the packed halves by
+// v_fma_mix_f32); the element's 8 bytes become (h_re, h_im | l_re, l_im)
+__device__ __forceinline__ c64 f16_terms(c64 v, int sc) {
+  const float x0 = ldexpf(v.re, sc), x1 = ldexpf(v.im, sc);
+  const f16x2 hv = {(_Float16)x0, (_Float16)x1};
+  const uint32_t h = __builtin_bit_cast(uint32_t, hv);
+  float r0, r1;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r0) : "v"(x0), "v"(h));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r1) : "v"(x1), "v"(h));
+  const f16x2 lv = {(_Float16)r0, (_Float16)r1};
+  return c64{__uint_as_float(h), __uint_as_float(__builtin_bit_cast(uint32_t, lv))};
+}
 
 // uniform base + zero-extended 32-bit lane byte offset: global_load/store with an SGPR-pair base
 // and one VGPR offset shared by every register slot (no 64-bit VGPR address per slot)
@@ -101,6 +123,12 @@ __device__ __forceinline__ f2v pmac(f2v acc, f2v a, f2v b) {
 
 template <typename T>
 __device__ __forceinline__ void mac(T& acc, const T& a, const T& b) {
+#if defined(TQ_S2_DIAG) && TQ_S2_DIAG == 1
+  // development diagnostic: no arithmetic (the data movement of every pass stays)
+  (void)b;
+  acc = a;
+  return;
+#endif
   if constexpr (std::is_same<T, c64>::value) {
     const f2v r = pmac(f2v{acc.re, acc.im}, f2v{a.re, a.im}, f2v{b.re, b.im});
     acc = c64{r.x, r.y};
@@ -403,10 +431,20 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   auto track = [&](const T& v) {
     if constexpr (kC64) vmax = fmaxf(vmax, fmaxf(fabsf(v.re), fabsf(v.im)));
   };
+  // S2Op::split_sc: the stored form is the f16 terms (uniform branch)
+  const bool split = kC64 && op.split_sc != nullptr;
+  const int split_sc = split ? *op.split_sc : 0;
+  auto stored = [&](const T& v) -> T {
+    if constexpr (kC64) {
+      if (split) return f16_terms(v, split_sc);
+    }
+    return v;
+  };
   __syncthreads();
   TQ_TS(1);
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
   const int ngates = ds->ngates;
+  const int epi = ds->epi;   // S2Desc::epi (read before the tile overwrites the descriptor copy)
   // ---- per-thread part of the load / store enumerations (low LOG_NT chunk bits); threads
   // beyond a small chunk duplicate element tid % n (same value to the same place)
   int64_t ldm = 0, stm = 0;
@@ -588,7 +626,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
             for (int q = 0; q < 4; ++q) {
               T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + q]), sto);
               const T v = use_beta ? scale_add(t[q], *p, beta) : t[q];
-              *p = v;
+              TQ_ST(p, stored(v));
               if constexpr (TRK) track(v);
             }
           }
@@ -601,13 +639,56 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
           TQ_BY_COUNT(4, rout, {
             T* p = lane_at(Y + uniform(base + hot.st_hm[r]), sto);
             const T v = use_beta ? scale_add(t[r], *p, beta) : t[r];
-            *p = v;
+            TQ_ST(p, stored(v));
             if constexpr (TRK) track(v);
           });
         }
       }
     };
-    if (kC64 && amax) store_chunk(std::true_type{});
+    // S2Desc::epi: the last gate is applied here, in registers -- a thread reads the K inputs of
+    // a group (slots r0 .. r0+K-1 of the pre-gate tile) and stores its N outputs (slots r0 ..
+    // r0+N-1); the coefficients are wave-uniform (scalar registers)
+    auto store_epi = [&](auto kt, auto nt, auto tracked) {
+      constexpr int K = decltype(kt)::value, N = decltype(nt)::value;
+      constexpr bool TRK = decltype(tracked)::value;
+      const T* ce = cf + (epi - 1) * kCf;
+      T c[K * N];
+#pragma unroll
+      for (int q = 0; q < K * N; ++q) c[q] = uniform(ce[q]);
+      for (int r0 = 0; r0 < rout; r0 += N) {
+        T x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[k] = buf[sta ^ hot.st_ha[r0 + k]];
+        if (st_lane) {
+#pragma unroll
+          for (int n = 0; n < N; ++n) {
+            T acc = tzero<T>();
+#pragma unroll
+            for (int k = 0; k < K; ++k) mac(acc, x[k], c[k * N + n]);
+            T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + n]), sto);
+            const T v = use_beta ? scale_add(acc, *p, beta) : acc;
+            TQ_ST(p, stored(v));
+            if constexpr (TRK) track(v);
+          }
+        }
+        asm volatile("" ::: "memory");
+      }
+    };
+    auto store_epi_kn = [&](auto tracked) {
+      using std::integral_constant;
+#define TQ_EPI(k, n) \
+  case k * 16 + n: store_epi(integral_constant<int, k>{}, integral_constant<int, n>{}, tracked); break;
+      const int32_t* gm = gmeta + (epi - 1) * kGm;
+      switch (gm[kGmK] * 16 + gm[kGmN]) {
+        TQ_EPI(1, 2) TQ_EPI(1, 4) TQ_EPI(1, 8) TQ_EPI(2, 2) TQ_EPI(2, 4) TQ_EPI(2, 8) TQ_EPI(4, 4)
+        default: break;   // the plan compiler only emits these (K <= N, K * N <= 16)
+      }
+#undef TQ_EPI
+    };
+    if (epi) {
+      if (kC64 && amax) store_epi_kn(std::true_type{});
+      else store_epi_kn(std::false_type{});
+    } else if (kC64 && amax) store_chunk(std::true_type{});
     else store_chunk(std::false_type{});
     __syncthreads();  // every wave has read the tile
     if (ch == lb) TQ_TS(5);

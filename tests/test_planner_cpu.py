@@ -210,3 +210,17 @@ def test_sweep2_lane_offsets_stay_32bit(n_legs, want_s2):
     e = HipContractExpression(eq, *shapes, optimize=path)
     d = e.plan(torch.complex64).describe()
     assert ("SWEEP2" in d) == want_s2, d
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_boundary_gemm_takes_presplit_operands(cfg):
+    """The boundary GEMM of C3 / C4 is a pre-split candidate: both operands come from per-slice
+    sweep2 ops that nothing else reads, so those ops may store the f16 terms the GEMM consumes
+    (tq_plan.cpp Compiler::assign_amax); the operand-max words stay in place for the check."""
+    e, p = _plan(config_task(cfg))
+    assert p.query("n_presplit") == 1
+    gemm = [l for l in p.describe().splitlines() if " GEMM " in l]
+    assert len(gemm) == 1 and "presplit" in gemm[0] and "amax<-" in gemm[0]
+    # complex128 plans have no f16 path and no candidates
+    e2, p2 = _plan(config_task(cfg), "complex128")
+    assert p2.query("n_presplit") == 0
