@@ -870,6 +870,13 @@ class Compiler {
     }();
     return v;
   }
+  static int s2_min_logc() {   // narrowest chunk (log2 columns) of the small-tensor rule
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_MINLC");
+      return e ? std::max(0, std::min(5, atoi(e))) : 2;
+    }();
+    return v;
+  }
   static bool s2_blocks_enabled() {
     static const int v = [] {
       const char* e = getenv("TQ_S2_BLOCKS");
@@ -1040,7 +1047,7 @@ class Compiler {
     if (const int mc = s2_min_chunks(); mc > 1) {
       int lg = 0;
       while ((2 << lg) <= mc) ++lg;
-      lc = std::min(lc, std::max(std::min(2, d.colbits), d.colbits - lg));
+      lc = std::min(lc, std::max(std::min(s2_min_logc(), d.colbits), d.colbits - lg));
     }
     d.logC = lc;
     d.nchunks = int64_t(1) << (d.colbits - lc);

@@ -15,4 +15,10 @@ out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
 for _ in range(4):
     expr(*ops, out=out)
 torch.cuda.synchronize()
-print("ok", float(out.abs().max()))
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(10):
+    expr(*ops, out=out)
+e1.record()
+torch.cuda.synchronize()
+print(f"ms_per_execute {e0.elapsed_time(e1) / 10:.3f} max|amp| {float(out.abs().max()):.6e}")
