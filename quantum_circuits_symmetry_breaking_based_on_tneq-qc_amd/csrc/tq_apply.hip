@@ -79,6 +79,19 @@ axpy_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ y, float bf, dou
   }
 }
 
+// y[i] = sum_{j < nl} y[i + j * stride]: the slice lanes' copies of a per-slice result summed
+// into lane 0's (Plan::lanes; the real / complex parts are independent, so R words suffice)
+template <typename R>
+__global__ void __launch_bounds__(kThreads)
+lane_sum_kernel(int64_t n, R* __restrict__ y, int64_t stride, int nl) {
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kThreads) {
+    R v = y[i];
+    for (int j = 1; j < nl; ++j) v += y[i + j * stride];
+    y[i] = v;
+  }
+}
+
 template <typename T>
 int apply_t(int64_t O, int64_t K1, int64_t M, int64_t K2, int64_t I, int64_t N, const void* S,
             const void* G, const int32_t* gidx, void* C, double beta, hipStream_t stream) {
@@ -130,6 +143,23 @@ int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_
   }
   set_error("apply: bad dtype");
   return TQ_ERR_INVALID;
+}
+
+int lane_sum_launch(int dtype, int64_t n, void* y, int64_t stride, int nl, hipStream_t stream) {
+  if (n == 0 || nl <= 1) return TQ_OK;
+  const int w = (dtype == TQ_C64 || dtype == TQ_C128) ? 2 : 1;   // R words per element
+  const int64_t nr = n * w;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nr + kThreads - 1) / kThreads, 4096));
+  if (dtype == TQ_F32 || dtype == TQ_C64)
+    hipLaunchKernelGGL((lane_sum_kernel<float>), dim3(blocks), dim3(kThreads), 0, stream, nr, (float*)y, stride * w, nl);
+  else if (dtype == TQ_F64 || dtype == TQ_C128)
+    hipLaunchKernelGGL((lane_sum_kernel<double>), dim3(blocks), dim3(kThreads), 0, stream, nr, (double*)y, stride * w, nl);
+  else {
+    set_error("lane_sum: bad dtype");
+    return TQ_ERR_INVALID;
+  }
+  TQ_HIP(hipGetLastError());
+  return TQ_OK;
 }
 
 int axpy_launch(int dtype, int64_t n, const void* x, void* y, double beta, hipStream_t stream) {

@@ -223,6 +223,7 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "graph_builds") return P.graph_builds;
   if (k == "graph_launches") return P.graph_launches;
   if (k == "n_presplit") return P.n_ps;
+  if (k == "lanes") return P.lanes;
   if (k == "presplit_fallbacks") return P.ps_fallbacks;
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;

@@ -126,6 +126,8 @@ int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_
                  const void* S, const void* G, const int32_t* gidx, void* C, double beta,
                  hipStream_t stream);
 int axpy_launch(int dtype, int64_t n, const void* x, void* y, double beta, hipStream_t stream);
+// y[i] = sum_{j < nl} y[i + j * stride] (elements), i < n: slice lanes summed into lane 0
+int lane_sum_launch(int dtype, int64_t n, void* y, int64_t stride, int nl, hipStream_t stream);
 // measurement data (tq_data.hip)
 int hermite_launch(int dtype, int64_t n, int K, const double* x, const double* w, void* phi,
                    void* mx, hipStream_t stream);

@@ -97,7 +97,9 @@ std::string modes_str(const std::vector<int>& m) {
 
 class Compiler {
  public:
-  Compiler(Plan& P) : P_(P) {}
+  // lanes_hint > 1: the plan will run its slices in batches of that many lanes, so a
+  // slice-dependent sweep op needs only min_chunks / lanes chunks to fill the GPU
+  Compiler(Plan& P, int lanes_hint = 1) : P_(P), lanes_hint_(lanes_hint) {}
 
   int run(int n_inputs, const int32_t* in_ranks, const int32_t* in_modes, const int64_t* in_ext,
           const int64_t* in_strides, int out_rank, const int32_t* out_modes, int n_steps,
@@ -228,6 +230,50 @@ class Compiler {
       const int64_t pbase[2] = {0, al(pinned_arenas_[0].peak())};
       P_.pinned_base = (size_t)al(abase[1] + arenas_[1].peak());
       P_.arena_bytes = P_.pinned_base + (size_t)(pbase[1] + pinned_arenas_[1].peak());
+      P_.lane0_bytes = P_.arena_bytes;
+      P_.lanes = 1;
+      if (const int want = slice_lanes(); P_.n_slices > 1 && want > 1 && P_.pinned_base > 0 &&
+                                          P_.pinned_base <= kLaneArenaMax)
+        P_.lanes = (int)std::min<int64_t>(want, P_.n_slices);
+      P_.lane_phys = (size_t)al((int64_t)(P_.arena_bytes - P_.pinned_base));
+      P_.lane_stride = P_.pinned_base;
+      P_.lane_ws_off = P_.lane_phys + (size_t)P_.lanes * P_.lane_stride;
+      P_.arena_bytes = P_.lane_ws_off;   // + the lane-batched GEMM workspace (run(), after lowering)
+      // lane-batched GEMMs and their shared workspace
+      if (P_.lanes > 1) {
+        size_t wsmax = 0;
+        for (auto& op : P_.ops) {
+          const bool okab = (op.a.kind == BUF_ARENA || op.a.kind == BUF_PINNED) &&
+                            (op.b.kind == BUF_ARENA || op.b.kind == BUF_PINNED);
+          if (op.kind != OP_GEMM || op.invariant || op.batch != 1 || op.writes_output || !okab ||
+              op.c.kind != BUF_ARENA || (P_.lane_stride / P_.esz) % 2)
+            continue;
+          op.lane_batch = true;
+          op.note += " lanes";
+          wsmax = std::max(wsmax, gemm_workspace(P_.dtype, op.M, op.N, op.K, P_.lanes));
+        }
+        // a lane-batched GEMM whose result only an output permute reads: sum the lanes first
+        for (size_t i = 0; i < P_.ops.size(); ++i) {
+          Op& g = P_.ops[i];
+          if (!g.lane_batch) continue;
+          const int64_t lo = g.c.off, hi = g.c.off + g.nc;
+          int reader = -1, nread = 0;
+          for (size_t k = i + 1; k < P_.ops.size(); ++k) {
+            const Op& o = P_.ops[k];
+            auto rd = [&](const BufRef& r, int64_t n) { return r.kind == BUF_ARENA && r.off < hi && lo < r.off + n; };
+            if (rd(o.a, o.na) || rd(o.b, o.nb) || (o.kind == OP_AXPY && rd(o.c, o.nc))) { ++nread; reader = (int)k; }
+            for (auto& sg : o.sgates) if (rd(sg.g, std::max<int64_t>(sg.n, 1))) ++nread;
+            if (o.c.kind == BUF_ARENA && o.c.off < hi && lo < o.c.off + o.nc) break;   // overwritten
+          }
+          if (nread != 1) continue;
+          Op& pm = P_.ops[reader];
+          if (pm.kind != OP_PERMUTE || !pm.writes_output || pm.invariant || pm.a.off != g.c.off) continue;
+          g.lane_sum = pm.lane_once = true;
+          g.note += " lane-sum";
+        }
+        P_.lane_ws_bytes = (size_t)al((int64_t)wsmax);
+        P_.arena_bytes += P_.lane_ws_bytes;
+      }
       const int64_t esz = (int64_t)P_.esz;
       auto fix = [&](BufRef& b) {
         if (b.kind == BUF_ARENA) b.off += abase[b.region] / esz;
@@ -870,6 +916,15 @@ class Compiler {
     }();
     return v;
   }
+  // slices per batch when the per-slice working set is small (TQ_SLICE_LANES, default 8; 1 = off)
+  static constexpr size_t kLaneArenaMax = size_t(32) << 20;
+  static int slice_lanes() {
+    static const int v = [] {
+      const char* e = getenv("TQ_SLICE_LANES");
+      return e ? std::max(1, std::min(16, atoi(e))) : 8;
+    }();
+    return v;
+  }
   static int s2_min_logc() {   // narrowest chunk (log2 columns) of the small-tensor rule
     static const int v = [] {
       const char* e = getenv("TQ_S2_MINLC");
@@ -1044,7 +1099,8 @@ class Compiler {
     lc = std::min(lc, d.colbits);
     // small tensors: narrower chunks, so that the op still spreads over >= s2_min_chunks()
     // workgroups (a 2^19-element tensor with a 256-element tile has only 64 chunks of 32 columns)
-    if (const int mc = s2_min_chunks(); mc > 1) {
+    if (const int mc = (c.dep && lanes_hint_ > 1) ? std::max(1, s2_min_chunks() / lanes_hint_) : s2_min_chunks();
+        mc > 1) {
       int lg = 0;
       while ((2 << lg) <= mc) ++lg;
       lc = std::min(lc, std::max(std::min(s2_min_logc(), d.colbits), d.colbits - lg));
@@ -1663,6 +1719,7 @@ class Compiler {
   }
 
   Plan& P_;
+  int lanes_hint_ = 1;
   bool cplx_ = false;
   int n_inputs_ = 0;
   Chain chain_;
@@ -1691,8 +1748,19 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
   P = Plan{};
   P.dtype = dtype;
   Compiler c(P);
-  return c.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
-               path, n_sliced, sliced_modes);
+  TQ_TRY(c.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
+               path, n_sliced, sliced_modes));
+  if (P.lanes > 1) {
+    // slice lanes: compile again with wider chunks for the slice-dependent sweeps (the lanes of
+    // a batch share their launches); kept if the second plan runs with the same lanes
+    Plan Q{};
+    Q.dtype = dtype;
+    Compiler c2(Q, P.lanes);
+    if (c2.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
+               path, n_sliced, sliced_modes) == TQ_OK && Q.lanes == P.lanes)
+      P = std::move(Q);
+  }
+  return TQ_OK;
 }
 
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
@@ -1892,30 +1960,51 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     if (!accumulate && P.out_numel) TQ_HIP(hipMemsetAsync(out, 0, P.out_numel * esz, stream));
     return TQ_OK;
   }
-  for (int64_t sl = s_begin; sl < s_end; sl += s_step) {
-    // decode slice id (row-major over sliced modes) -> per-input element offsets
-    std::vector<int64_t> idx(ns);
-    int64_t rem = sl;
-    for (int q = ns - 1; q >= 0; --q) { idx[q] = rem % P.sliced_ext[q]; rem /= P.sliced_ext[q]; }
-    for (int i = 0; i < P.n_inputs; ++i) {
-      int64_t o = 0;
-      for (int q = 0; q < ns; ++q) o += idx[q] * P.inputs[i].slice_stride[q];
-      in_off[i] = o;
+  // Slices run in batches of P.lanes (slice lanes, Plan::lanes): lane j owns its own copy of the
+  // per-slice arena part, the batch's sweep2 levels share launches across lanes, other ops run
+  // lane by lane in lane order (so output accumulation keeps its order)
+  const int64_t nlanes = std::max(1, P.lanes);
+  std::vector<std::vector<int64_t>> lane_in_off;
+  std::vector<int64_t> lane_sl;
+  int cur = 0;   // lane the launches below address
+  for (int64_t s0 = s_begin; s0 < s_end; s0 += s_step * nlanes) {
+    lane_sl.clear();
+    lane_in_off.clear();
+    for (int64_t sl = s0; sl < s_end && (int64_t)lane_sl.size() < nlanes; sl += s_step) {
+      // decode slice id (row-major over sliced modes) -> per-input element offsets
+      std::vector<int64_t> idx(ns);
+      int64_t rem = sl;
+      for (int q = ns - 1; q >= 0; --q) { idx[q] = rem % P.sliced_ext[q]; rem /= P.sliced_ext[q]; }
+      for (int i = 0; i < P.n_inputs; ++i) {
+        int64_t o = 0;
+        for (int q = 0; q < ns; ++q) o += idx[q] * P.inputs[i].slice_stride[q];
+        in_off[i] = o;
+      }
+      lane_sl.push_back(sl);
+      lane_in_off.push_back(in_off);
     }
+    const int64_t sl = lane_sl[0];
+    cur = 0;
     auto ptr = [&](const BufRef& b) -> char* {
       switch (b.kind) {
-        case BUF_INPUT: return (char*)inputs[b.index] + (in_off[b.index] + b.off) * esz;
-        case BUF_ARENA: return (char*)P.d_arena + b.off * esz;
-        case BUF_PINNED: return (char*)P.d_arena + P.pinned_base + b.off * esz;
+        case BUF_INPUT: return (char*)inputs[b.index] + (lane_in_off[cur][b.index] + b.off) * esz;
+        case BUF_ARENA: return (char*)P.d_arena + P.lane_phys + (size_t)cur * P.lane_stride + b.off * esz;
+        case BUF_PINNED: return (char*)P.d_arena + b.off * esz;
         case BUF_OUTPUT: return (char*)out + b.off * esz;
       }
       return nullptr;
     };
-    const double beta_out = first ? 0.0 : 1.0;
+    // the first slice of a non-accumulating call overwrites the output, the others add
+    double beta_out = (first && cur == 0) ? 0.0 : 1.0;
+    auto set_lane = [&](int j) {
+      cur = j;
+      beta_out = (first && cur == 0) ? 0.0 : 1.0;
+    };
     auto amax_word = [&](int w) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.amax_off) + w; };
     // scale word of per-slice max word w; window flag of slice q
     auto sc_word = [&](int w) { return reinterpret_cast<int32_t*>((char*)P.d_tables + P.sc_off) + (w - P.n_amax_once); };
     auto bad_word = [&](int64_t q) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.bad_off) + q; };
+    int lane_gemm = 1;   // > 1: the GEMM launch below covers that many lanes
     auto launch_one = [&](const Op& op, hipStream_t st) -> int {
       const double beta = op.writes_output ? beta_out : 0.0;
       switch (op.kind) {
@@ -1929,7 +2018,17 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           if (pre) {
             ps.sc_a = sc_word(op.amax_a);
             ps.sc_b = sc_word(op.amax_b);
-            ps.bad = bad_word(sl);
+            ps.bad = bad_word(lane_sl[cur]);
+          }
+          if (lane_gemm > 1) {   // every lane of the batch in one launch (Op::lane_batch)
+            const int64_t ls = (int64_t)(P.lane_stride / esz);
+            TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, lane_gemm, ptr(op.a),
+                               op.lda, op.a.kind == BUF_ARENA ? ls : 0, ptr(op.b), op.ldb,
+                               op.b.kind == BUF_ARENA ? ls : 0, beta, ptr(op.c), op.ldc, ls,
+                               (char*)P.d_arena + P.lane_ws_off, P.lane_ws_bytes, st,
+                               op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
+                               op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, nullptr));
+            break;
           }
           TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
                              op.lda, op.sA, ptr(op.b), op.ldb, op.sB, beta, ptr(op.c), op.ldc, op.sC,
@@ -2022,15 +2121,25 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           P.ev_free.pop_back();
         }
         ev.kind = pkind; ev.flops = 0; ev.bytes = 0;
-        for (int j : grp) { ev.flops += P.ops[j].flops; ev.bytes += P.ops[j].bytes; }
+        for (int j : grp) { ev.flops += P.ops[j].flops * lane_gemm; ev.bytes += P.ops[j].bytes * lane_gemm; }
         TQ_HIP(hipEventRecord(ev.a, stream));
       }
+      bool lanes_merge = op0.kind == OP_SWEEP2 && lane_sl.size() > 1 && !op0.invariant;
+      for (int j : grp) lanes_merge = lanes_merge && !P.ops[j].writes_output;
       if (op0.kind == OP_SWEEP2) {
+        // (lane, op) pairs of this level: every lane's ops when the level is merged across the
+        // batch, else the current lane's; at most kS2MaxOps per launch
+        std::vector<std::pair<int, int>> items;
+        for (int j = 0; j < (lanes_merge ? (int)lane_sl.size() : 1); ++j)
+          for (int q : grp) items.push_back({lanes_merge ? j : cur, q});
+        const int keep = cur;
+        for (size_t i0 = 0; i0 < items.size(); i0 += kS2MaxOps) {
         S2Launch L;
-        L.nops = (int)grp.size();
+        L.nops = (int)std::min<size_t>(kS2MaxOps, items.size() - i0);
         int blocks = 0;
         for (int q = 0; q < L.nops; ++q) {
-          const Op& op = P.ops[grp[q]];
+          set_lane(items[i0 + q].first);
+          const Op& op = P.ops[items[i0 + q].second];
           S2Op& o = L.op[q];
           o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[op.stab]);
           o.X = ptr(op.a);
@@ -2052,6 +2161,8 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
         }
         TQ_TRY(sweep2_launch(P.dtype, L, stream));
+        }
+        set_lane(keep);
       } else {
         TQ_TRY(launch_one(op0, stream));
       }
@@ -2065,11 +2176,41 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
       for (auto& grp : P.sched_once) TQ_TRY(launch(grp));
     }
+    // per-slice max words: shared by the lanes of a batch (max-ed over all of them, an upper
+    // bound of every lane's operand)
     if (P.n_amax_slice && P.run_mode)   // scales from the previous slice's max, then max = 0
       TQ_TRY(presplit_prep_launch(amax_word(P.n_amax_once), sc_word(P.n_amax_once), P.n_amax_slice, stream));
     else if (P.n_amax_slice)
       TQ_HIP(hipMemsetAsync(amax_word(P.n_amax_once), 0, P.n_amax_slice * sizeof(uint32_t), stream));
-    for (auto& grp : P.sched_slice) TQ_TRY(launch(grp));
+    bool lanes_summed = false;   // this batch's lanes were summed into lane 0 (Op::lane_sum)
+    for (auto& grp : P.sched_slice) {
+      const Op& op0 = P.ops[grp[0]];
+      bool merged = op0.kind == OP_SWEEP2;
+      for (int j : grp) merged = merged && !P.ops[j].writes_output;
+      if (merged || lane_sl.size() == 1) {
+        set_lane(0);
+        TQ_TRY(launch(grp));
+      } else if (op0.kind == OP_GEMM && op0.lane_batch && !P.run_mode) {
+        set_lane(0);
+        lane_gemm = (int)lane_sl.size();
+        const int rc = launch(grp);
+        lane_gemm = 1;
+        TQ_TRY(rc);
+        if (op0.lane_sum) {
+          TQ_TRY(lane_sum_launch(P.dtype, op0.nc, ptr(op0.c), (int64_t)(P.lane_stride / esz),
+                                 (int)lane_sl.size(), stream));
+          lanes_summed = true;
+        }
+      } else if (op0.lane_once && lanes_summed) {
+        set_lane(0);
+        TQ_TRY(launch(grp));
+      } else {
+        for (int j = 0; j < (int)lane_sl.size(); ++j) {
+          set_lane(j);
+          TQ_TRY(launch(grp));
+        }
+      }
+    }
     first = false;
   }
   return TQ_OK;

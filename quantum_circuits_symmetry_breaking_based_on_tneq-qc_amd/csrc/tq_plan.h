@@ -72,6 +72,12 @@ struct Op {
   // (ps_cand); its producers (ps_gemm = that GEMM) then store the terms (S2Op::split_sc)
   bool ps_cand = false;
   int ps_gemm = -1;
+  // per-slice GEMM on lane-local (or pinned) operands: the lanes of a batch run as ONE batched
+  // launch (strides = Plan::lane_stride, workspace at Plan::lane_ws_off)
+  bool lane_batch = false;
+  // lane_sum (a lane-batched GEMM): its result is read only by one output permute, so the
+  // lanes' results are summed into lane 0's and that permute (lane_once) runs once per batch
+  bool lane_sum = false, lane_once = false;
   // element counts of a / b / c / ws (hazard analysis of the launch schedule)
   int64_t na = 0, nb = 0, nc = 0, nws = 0;
   // bookkeeping
@@ -119,6 +125,16 @@ struct Plan {
   int64_t ps_fallbacks = 0;   // slices re-run on the split path (operand max left the window)
   size_t arena_bytes = 0;
   size_t pinned_base = 0;             // pinned (hoisted, slice-invariant) results live above this
+  // slice lanes: slices run in batches of `lanes`; lane j > 0 has its own copy of the per-slice
+  // part [0, pinned_base) at lane0_bytes + (j-1) * pinned_base (arena_bytes includes the copies).
+  // Small per-slice working sets only (C3: 64 latency-bound slices), 1 otherwise (C4)
+  int lanes = 1;
+  size_t lane0_bytes = 0;
+  // physical arena: [pinned part][lane 0][lane 1]...[lane-batched GEMM workspace]; lane j's copy
+  // of [0, pinned_base) starts at lane_phys + j * lane_stride (a uniform stride, so a per-slice
+  // GEMM of all lanes is ONE batched launch); the logical offsets used by the compiler's
+  // analyses are unchanged (arena [0, pinned_base), pinned above)
+  size_t lane_phys = 0, lane_stride = 0, lane_ws_off = 0, lane_ws_bytes = 0;
   void* d_arena = nullptr;
   void* d_tables = nullptr;
   bool owns_device = false;
