@@ -145,42 +145,29 @@ def permute_probe(dev, rank: int = 26, reps: int = 5):
             "bit_exact": ok}
 
 
-def c5_train(dev, with_cpu: bool = True, steps: int = 5, warmup: int = 2):
+def c5_train(dev, with_cpu: bool = True, steps: int = 20, warmup: int = 5):
     """Secondary line (BASELINE.json configs[4], C5): the symmetry-breaking training step —
     8 pruning candidates x (core-only forward, fidelity loss, reverse-mode backward, SGDG) in
-    complex128 — next to the same step on the host CPU (scripts/c5_bench.py)."""
-    import importlib.util
-    import random
-    import torch
-    spec = importlib.util.spec_from_file_location("c5_bench", os.path.join(ROOT, "scripts", "c5_bench.py"))
-    cb = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(cb)
-    random.seed(0)
-    target, cands = cb.setup(dev)
-    # one stream per candidate (independent fits; tests/test_c5_streams_gpu.py: identical results)
-    streams = [torch.cuda.Stream(dev) for _ in cands]
-    for _ in range(warmup):
-        cb.gpu_step(target, cands, streams)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        cb.gpu_step(target, cands, streams)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    r = {"metric": "candidate training steps/s (forward + backward + SGDG), C5 ansatz, 8 candidates",
-         "value": len(cands) / dt, "unit": "candidate-steps/s", "ms_per_step": dt * 1e3, "steps": steps,
-         "dtype": "c128", "cores_per_candidate": len(cands[0][1]), "streams": len(streams),
-         "amplitudes_per_forward": int(math.prod(cands[0][0].out_shape)),
-         "bound": "latency (2^16-element tensors; ~100 dependent pairwise launches per candidate-step; "
-                  "the 8 candidates' chains overlap on 8 streams)"}
-    if with_cpu:
-        torch.set_num_threads(min(16, os.cpu_count() or 1))
-        secs, n = cb.cpu_step_sample(target.cpu().numpy(), cands, 1)
-        r["cpu_baseline"] = {"value": n / secs, "unit": "candidate-steps/s", "cores": torch.get_num_threads(),
-                             "kind": "port", "cpu_model": _cpu_model(),
-                             "sample": f"{n} candidate-steps: torch CPU pairwise tensordot along the same "
-                                       "path + autograd + the oracle's SGDG restatement, complex128"}
-    return r
+    complex128, each candidate on its own stream — next to the same step on the host CPU.
+    Runs scripts/c5_bench.py in a child process (started without exec): a fresh caching
+    allocator, so the candidates' buffers (and the hipGraphs keyed on their pointers) settle
+    during the warmup instead of inheriting the C4 run's pool."""
+    import subprocess
+    del dev
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "c5_bench.py"), "--steps", str(steps),
+           "--warmup", str(warmup), "--cpu-steps", "1" if with_cpu else "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    out = {"metric": "candidate training steps/s (forward + backward + SGDG), C5 ansatz, 8 candidates",
+           "value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": steps,
+           "warmup": warmup, "dtype": d["dtype"], "cores_per_candidate": d["cores_per_candidate"],
+           "streams": d.get("streams", 1), "amplitudes_per_forward": d["amplitudes_per_forward"],
+           "bound": "latency (2^16-element tensors; ~100 dependent pairwise launches per candidate-step; "
+                    "the 8 candidates' chains overlap on 8 streams)"}
+    if "cpu_baseline" in d:
+        out["cpu_baseline"] = dict(d["cpu_baseline"], cpu_model=_cpu_model())
+    return out
 
 
 def alt_gemm(args, var: str, desc: str):

@@ -232,9 +232,11 @@ class Compiler {
       P_.arena_bytes = P_.pinned_base + (size_t)(pbase[1] + pinned_arenas_[1].peak());
       P_.lane0_bytes = P_.arena_bytes;
       P_.lanes = 1;
-      if (const int want = slice_lanes(); P_.n_slices > 1 && want > 1 && P_.pinned_base > 0 &&
-                                          P_.pinned_base <= kLaneArenaMax)
-        P_.lanes = (int)std::min<int64_t>(want, P_.n_slices);
+      if (const int want = slice_lanes(); P_.n_slices > 1 && want > 1 && P_.pinned_base > 0) {
+        const int64_t cap = std::min<int64_t>({(int64_t)want, P_.n_slices,
+                                               (int64_t)(lane_arena_budget() / P_.pinned_base)});
+        while (P_.lanes * 2 <= cap) P_.lanes *= 2;   // a power of two
+      }
       P_.lane_phys = (size_t)al((int64_t)(P_.arena_bytes - P_.pinned_base));
       P_.lane_stride = P_.pinned_base;
       P_.lane_ws_off = P_.lane_phys + (size_t)P_.lanes * P_.lane_stride;
@@ -917,7 +919,15 @@ class Compiler {
     return v;
   }
   // slices per batch when the per-slice working set is small (TQ_SLICE_LANES, default 8; 1 = off)
-  static constexpr size_t kLaneArenaMax = size_t(32) << 20;
+  // arena the lane copies may add in total (TQ_LANE_ARENA_MB, default 6 GiB of the 288 GB):
+  // C3's 6-MiB per-slice part gets 8 lanes, C4's 1.1 GiB gets 4 (measured: 16.4 -> 15.9 ms/step)
+  static size_t lane_arena_budget() {
+    static const size_t v = [] {
+      const char* e = getenv("TQ_LANE_ARENA_MB");
+      return (size_t)(e ? std::max(0, atoi(e)) : 6144) << 20;
+    }();
+    return v;
+  }
   static int slice_lanes() {
     static const int v = [] {
       const char* e = getenv("TQ_SLICE_LANES");
@@ -2121,7 +2131,14 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           P.ev_free.pop_back();
         }
         ev.kind = pkind; ev.flops = 0; ev.bytes = 0;
-        for (int j : grp) { ev.flops += P.ops[j].flops * lane_gemm; ev.bytes += P.ops[j].bytes * lane_gemm; }
+        // a lane-batched GEMM or a sweep level merged across the batch's lanes does every lane's work
+        int mult = lane_gemm;
+        if (op0.kind == OP_SWEEP2 && lane_sl.size() > 1 && !op0.invariant) {
+          bool m = true;
+          for (int j : grp) m = m && !P.ops[j].writes_output;
+          if (m) mult = (int)lane_sl.size();
+        }
+        for (int j : grp) { ev.flops += P.ops[j].flops * mult; ev.bytes += P.ops[j].bytes * mult; }
         TQ_HIP(hipEventRecord(ev.a, stream));
       }
       bool lanes_merge = op0.kind == OP_SWEEP2 && lane_sl.size() > 1 && !op0.invariant;
