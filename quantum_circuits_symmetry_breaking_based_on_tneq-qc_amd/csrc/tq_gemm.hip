@@ -38,7 +38,8 @@ static int env_int(const char* name) {
   const char* e = getenv(name);
   return e ? atoi(e) : 0;
 }
-// f16-split tile variant: 0 = 8 waves of 64 x 32 (default), 1 = 4 waves of 64 x 64, 2 = 4 waves of
+// f16-split tile variant: 0 = 8 waves of 64 x 32 (default), 1 = 4 waves of 64 x 64, 3 = the default
+// tile on a 4-slot LDS ring (one barrier per two K-steps), 2 = 4 waves of
 // 64 x 64 with Gauss's 3-multiplication product (measurements: DESIGN.md §3)
 static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR")};
 int gemm_f16_var() { return g_gemm_f16_var.load(std::memory_order_relaxed); }
@@ -76,7 +77,7 @@ bool gemm_configure(const char* key, int64_t v) {
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16_var") {
-    if (v < 0 || v > 2) return false;
+    if (v < 0 || v > 3) return false;
     g_gemm_f16_var = (int)v;
     return true;
   }
@@ -640,8 +641,12 @@ namespace xbf {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_, bool G3_ = false>
+template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_, bool G3_ = false,
+          int SLOTS_ = 2>
 struct Tile {
+  // LDS slots of a K-step each: 2 = double buffer, one barrier per K-step; 4 = a ring in which a
+  // step's split lands two steps ahead, one barrier per TWO K-steps
+  static constexpr int SLOTS = SLOTS_;
   // ILV: the scheduler is told to interleave the split (VALU, LDS stores) with the MFMAs
   static constexpr bool ILV = ILV_;
   // G3: Gauss's 3-multiplication product (planes re, im, re + im per term; 3 accumulator sets)
@@ -657,7 +662,7 @@ struct Tile {
   // split task per thread: 2 rows x KPT consecutive k of one operand
   static constexpr int KPT = 16 * BM / NT;
   static_assert(BM == BN && (KPT == 4 || KPT == 8), "task split");
-  static_assert(2 * BUF <= 160 * 1024, "LDS");
+  static_assert(SLOTS * BUF <= 160 * 1024, "LDS");
 };
 // 8 waves (two per SIMD) of 64 x 32, block 128 x 128, 64 accumulators per wave; 4-k split tasks
 // (ds_write_b64).  bf16: 3 terms, 2 x 48 KiB LDS; f16: 2 terms, 2 x 32 KiB.
@@ -670,6 +675,8 @@ using TileH4 = Tile<2, 2, 2, 2, 2, 4, true>;
 // f16, Gauss 3M (TQ_GEMM_F16_VAR=2): P1 = Ar Br, P2 = Ai Bi, P3 = (Ar + Ai)(Br + Bi), 9 MFMAs per
 // complex tile-step instead of 12; 4 waves of 64 x 64 (3 x 64 accumulators), 3 staging sets
 using TileH4G = Tile<2, 2, 2, 2, 2, 3, true, true>;
+// f16, one barrier per two K-steps (TQ_GEMM_F16_VAR=3): the default tile on a 4-slot LDS ring
+using TileH2 = Tile<2, 4, 2, 1, 2, 4, true, false, 4>;
 
 __device__ __forceinline__ uint32_t hi16(float x) { return __float_as_uint(x) & 0xffff0000u; }
 // pack the bf16 held in the high halves of two dwords: lo <- a, hi <- b
@@ -857,7 +864,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   constexpr bool G3 = TL::G3;
   constexpr int NGRP = TL::NGRP, NACC = G3 ? 3 : 2;
   static_assert(TL::NTERM == SP::NTERM, "tile / split terms");
-  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  __shared__ __attribute__((aligned(16))) char lds[TL::SLOTS * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid % WMW, wn = wid / WMW;
@@ -1069,6 +1076,10 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   // measured slower at 512 with fewer staging sets.)
   FragA fa;
   FragB fb;
+  using I0_ = std::integral_constant<int, 0>;
+  using I1_ = std::integral_constant<int, 1>;
+  using I2_ = std::integral_constant<int, 2>;
+  using I3_ = std::integral_constant<int, 3>;
   auto body = [&](auto par, int t) {
     constexpr int P = decltype(par)::value;
     load(std::integral_constant<int, P % NSET>{}, t + NSET < nkt ? t + NSET : nkt - 1);
@@ -1097,6 +1108,49 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   using I5 = std::integral_constant<int, 5>;
 
   static_assert(NSET >= 2 && NSET <= 4, "register sets");
+  if constexpr (TL::SLOTS == 4) {
+    // 4-slot ring: K-step u is loaded 5 steps ahead into set u % 4, split at step u - 2 into
+    // slot u % 4, read and multiplied at step u; a barrier after every odd step -- between any
+    // slot's write (step u - 2) and read (step u), and between its read and next write, one of
+    // two consecutive steps is odd
+    static_assert(NSET == 4, "4 staging sets");
+    auto ck = [&](int u) { return u < nkt ? u : nkt - 1; };
+    load(I0_{}, 0);
+    load(I1_{}, ck(1));
+    load(I2_{}, ck(2));
+    load(I3_{}, ck(3));
+    store_stage(I0_{}, 0);
+    store_stage(I1_{}, 1);
+    load(I0_{}, ck(4));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    auto body4 = [&](auto par, int t) {
+      constexpr int P = decltype(par)::value;   // t % 4
+      load(std::integral_constant<int, (P + 1) % 4>{}, ck(t + 5));
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags(lds + P * BUF, fa, fb);
+      store_stage(std::integral_constant<int, (P + 2) % 4>{}, (P + 2) % 4);
+      mfmas(fa, fb);
+      if constexpr (TL::ILV) {
+        constexpr int NM = SP::NPAIR * TI * TJ * (G3 ? 3 : 4);
+        constexpr int NR = NGRP * NTM * (TI + TJ);
+        constexpr int NWR = 2 * NGRP * NTM;
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        Interleave<0, NM, 3, (NM / NWR > 0 ? NM / NWR : 1)>::run();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (P & 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    int t = 0;
+    for (; t + 4 <= nkt; t += 4) {
+      body4(I0_{}, t);
+      body4(I1_{}, t + 1);
+      body4(I2_{}, t + 2);
+      body4(I3_{}, t + 3);
+    }
+    if (t < nkt) body4(I0_{}, t);
+    if (t + 1 < nkt) body4(I1_{}, t + 1);
+    if (t + 2 < nkt) body4(I2_{}, t + 2);
+  } else {
   constexpr int U = NSET == 3 ? 6 : NSET;  // unroll: a multiple of NSET and of 2 (LDS halves)
   load(std::integral_constant<int, 0>{}, 0);
   load(std::integral_constant<int, 1>{}, nkt > 1 ? 1 : nkt - 1);
@@ -1123,6 +1177,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   }
   read_frags(lds + ((nkt - 1) & 1) * BUF, fa, fb);
   mfmas(fa, fb);  // step nkt - 1
+  }
 
   const bool partial = g.splits > 1;
   float* Cout = partial ? g.W + (((int64_t)split * g.batch + b) * g.M * g.N) * 2 : g.C + (int64_t)b * g.sC * 2;
@@ -1521,7 +1576,10 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.bad = ps->bad;
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitPre>), dim3((unsigned)nb),
                                dim3(xbf::TileH::NT), 0, stream, f);
-          } else if (var == 1)
+          } else if (var == 3)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH2, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH2::NT), 0, stream, f);
+          else if (var == 1)
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH4, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH4::NT), 0, stream, f);
           else if (var == 2)
