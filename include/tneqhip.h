@@ -67,12 +67,16 @@ int tq_device_synchronize(void);
  * gemm_bf16: a 2-term f16 split of the power-of-two-scaled operands, 12 MFMAs per complex
  * tile-step; 0 / env TQ_GEMM_F16=0: an exact 3-term bf16 split, 24 MFMAs), "gemm_f16_var" (f16
  * tile variant: 0 = 8 waves of 64x32, 1 = 4 waves of 64x64, 2 = 4 waves of 64x64 with Gauss's
- * 3-multiplication product; env TQ_GEMM_F16_VAR), "gemm_3m" (1: the f32-MFMA complex64 kernel uses Gauss's 3-multiplication
+ * 3-multiplication product, 3 = variant 0 on a 4-slot LDS ring, one barrier per two K-steps;
+ * env TQ_GEMM_F16_VAR), "gemm_presplit" (0 by default, env TQ_GEMM_PRESPLIT=1: a plan's per-slice
+ * sweep ops store the boundary GEMM's operands as f16 terms with a predicted scale, checked by
+ * the GEMM; a slice outside the window is re-run on the split path -- the execute call then
+ * synchronizes its stream), "presplit_bias" (testing: offset of the predicted scale), "gemm_3m" (1: the f32-MFMA complex64 kernel uses Gauss's 3-multiplication
  * product, env TQ_GEMM_3M=0 turns it off), "sweep" (fused multi-gate sweeps, env TQ_SWEEP),
  * "graphs" (plan execution through hipGraphs, env TQ_GRAPH).  -1 if unknown.  No reference
  * counterpart (the reference has no native layer); used for measurement reports. */
 int64_t tq_library_query(const char* key);
-/* Sets "gemm_bf16" / "gemm_f16" / "gemm_f16_var" / "gemm_3m" at run time (launches issued afterwards; a plan replaying a
+/* Sets "gemm_bf16" / "gemm_f16" / "gemm_f16_var" / "gemm_3m" / "gemm_presplit" / "presplit_bias" at run time (launches issued afterwards; a plan replaying a
  * captured hipGraph keeps the kernels it captured).  TQ_ERR_INVALID for other keys.  No
  * reference counterpart; used by tests and A/B measurements. */
 int tq_library_set(const char* key, int64_t value);
@@ -128,7 +132,10 @@ int tq_plan_create(tq_plan* plan, int dtype, int n_inputs, const int32_t* in_ran
 /* Queries (algorithmic counts): "n_slices", "arena_bytes", "table_bytes", "out_numel",
  * "flops" / "bytes_moved" (a whole execute over all slices), "flops_once" / "bytes_once"
  * (slice-invariant part, hoisted: run once per execute), "flops_slice" / "bytes_slice"
- * (per slice), "n_kernels", "n_ops_once", "n_gemm", "n_apply", "n_permute".  -1 if unknown. */
+ * (per slice), "n_kernels", "n_ops_once", "n_gemm", "n_apply", "n_permute", "lanes" (slices
+ * per batch: lane copies of the per-slice arena part within a 6-GiB budget, env TQ_SLICE_LANES /
+ * TQ_LANE_ARENA_MB), "n_presplit" (pre-split GEMM candidates), "presplit_fallbacks" (slices
+ * re-run on the split path so far).  -1 if unknown. */
 int64_t tq_plan_query(tq_plan plan, const char* key);
 /* Plan option: "graph" = 1 (default) replays the execute's launches from a captured hipGraph,
  * 0 launches them eagerly on the stream (use when the caller captures the stream itself). */
