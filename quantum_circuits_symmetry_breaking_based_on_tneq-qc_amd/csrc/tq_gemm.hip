@@ -1476,7 +1476,7 @@ int fast_c64_splits(int transA, int transB, int64_t M, int64_t N, int64_t K, int
 bool gemm_c64_presplit_ok(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
                           int64_t lda, int64_t ldb) {
   return gemm_presplit_enabled() && gemm_bf16() && gemm_f16() && gemm_f16_var() == 0 && !fast_disabled() &&
-         batch == 1 && lda % 2 == 0 && ldb % 2 == 0 && lda < (int64_t(1) << 24) && ldb < (int64_t(1) << 24) &&
+         batch >= 1 && lda % 2 == 0 && ldb % 2 == 0 && lda < (int64_t(1) << 24) && ldb < (int64_t(1) << 24) &&
          fast_c64_splits_t<xbf::TileX>(transA, transB, M, N, K, batch) > 0;
 }
 

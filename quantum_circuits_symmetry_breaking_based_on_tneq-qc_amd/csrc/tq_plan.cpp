@@ -1906,9 +1906,17 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
     const uint32_t* dbad = reinterpret_cast<const uint32_t*>((const char*)P.d_tables + P.bad_off);
     TQ_HIP(hipMemcpyAsync(P.h_bad, dbad, P.n_slices * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     TQ_HIP(hipStreamSynchronize(stream));
-    std::vector<int64_t> redo;
-    for (int64_t sl = s_begin; sl < s_end; sl += s_step)
-      if (P.h_bad[sl]) redo.push_back(sl);
+    // a lane-batched candidate GEMM flags its whole batch in the batch's first slice (the
+    // other lanes' words are not written): batches are consecutive groups of `lanes` slices
+    bool batched = false;
+    for (const Op& op : P.ops) batched = batched || (op.ps_cand && op.lane_batch);
+    std::vector<int64_t> redo, batch;
+    for (int64_t sl = s_begin; sl < s_end; sl += s_step * std::max(1, P.lanes)) {
+      batch.clear();
+      for (int64_t q = sl; q < s_end && (int64_t)batch.size() < std::max(1, P.lanes); q += s_step) batch.push_back(q);
+      for (int64_t q : batch)
+        if (batched ? P.h_bad[batch[0]] != 0 : P.h_bad[q] != 0) redo.push_back(q);
+    }
     P.run_mode = 0;
     for (int64_t sl : redo) TQ_TRY(plan_enqueue(P, inputs, out, sl, sl + 1, 1, 1, stream));
     P.ps_fallbacks += (int64_t)redo.size();
@@ -2032,12 +2040,13 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           }
           if (lane_gemm > 1) {   // every lane of the batch in one launch (Op::lane_batch)
             const int64_t ls = (int64_t)(P.lane_stride / esz);
+            // pre-split: one window flag for the batch, in its first slice's word
             TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, lane_gemm, ptr(op.a),
                                op.lda, op.a.kind == BUF_ARENA ? ls : 0, ptr(op.b), op.ldb,
                                op.b.kind == BUF_ARENA ? ls : 0, beta, ptr(op.c), op.ldc, ls,
                                (char*)P.d_arena + P.lane_ws_off, P.lane_ws_bytes, st,
                                op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
-                               op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, nullptr));
+                               op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, pre ? &ps : nullptr));
             break;
           }
           TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
@@ -2207,7 +2216,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       if (merged || lane_sl.size() == 1) {
         set_lane(0);
         TQ_TRY(launch(grp));
-      } else if (op0.kind == OP_GEMM && op0.lane_batch && !P.run_mode) {
+      } else if (op0.kind == OP_GEMM && op0.lane_batch) {
         set_lane(0);
         lane_gemm = (int)lane_sl.size();
         const int rc = launch(grp);
