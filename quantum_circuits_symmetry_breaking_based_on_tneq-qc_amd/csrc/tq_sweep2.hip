@@ -70,7 +70,7 @@ static_assert(kLut == 64, "lut layout shared with S2Desc::lut");
 // wall-clock stamps (100 MHz) at its phase boundaries
 // record: [0..6] phase stamps, [7] blocks|chunks, [8] first chunk's gate clocks,
 // [9..24] clock at the end of each pass of the first chunk, [25..40] pass kind (B<<16|K<<8|N)
-constexpr int kTsMax = 2048, kTsPh = 41;
+constexpr int kTsMax = 2048, kTsPh = 44;   // [41..43]: sub-stamps of the tables phase
 __device__ unsigned long long g_s2_ts[kTsMax][kTsPh];
 __device__ unsigned int g_s2_seq;
 #define TQ_TS(ph) do { if (ts_rec && threadIdx.x == 0) g_s2_ts[ts_idx][ph] = wall_clock64(); } while (0)
@@ -544,12 +544,14 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     const int64_t base = lane_bases ? lane64(cb_in, 0) : chunk_base(ch, ds->w_in);
     TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + ds->ld_hm[r]), ldo));
   }
+  TQ_TS(41);   // first chunk's loads issued
   // ---- gate coefficients -> LDS
   for (int i = tid; i < ngates * kCf; i += NT) {
     const int g = i / kCf, t = i % kCf;
     const S2Gate& gt = ds->gate[g];
     if (t < gt.K * gt.N) cf[i] = graw[g * kS2GateRaw + gt.gidx[t]];
   }
+  TQ_TS(42);   // coefficients staged
   // ---- per-chunk tables -> LDS
   for (int i = tid; i < kS2MaxSlots; i += NT) {
     hot.ld_hm[i] = ds->ld_hm[i];
@@ -567,6 +569,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   for (int i = tid; i < npass * 16; i += NT) pmeta[i] = ds->pmeta[i / 16][i % 16];
   constexpr int kSh = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;
   for (int i = tid; i < ngates * kLut; i += NT) lut[i] = ds->lut[i / kLut][i % kLut] << kSh;
+  TQ_TS(43);   // tables staged (before the barrier)
   __syncthreads();   // every wave is done with the descriptor copy: the tile may be written
   TQ_TS(2);
   // Chunk pipeline.  On this ISA one counter (vmcnt) covers loads and stores, and a wait for a

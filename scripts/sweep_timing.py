@@ -15,7 +15,7 @@ L = _lib.lib()
 f = L.tq_debug_sweep2_timing
 f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 f.restype = ctypes.c_int
-NREC, W = 2048, 41
+NREC, W = 2048, 44
 buf = (ctypes.c_ulonglong * (NREC * W))()
 task = config_task(sys.argv[1] if len(sys.argv) > 1 else "C4")
 expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
@@ -41,6 +41,14 @@ for r in a:
     print(f"start {(r[0]-t0)/100:8.2f} end {(r[6]-t0)/100:8.2f} | " + " ".join(f"{x:6.2f}" for x in ph)
           + f" | wgs {int(r[7]) >> 32} chunks {int(r[7]) & 0xffffffff} | gate clk {r[8] / max(ph[3], 1e-3) / 1e3:6.0f} MHz")
 print("sum per phase:", json.dumps(dict(zip(names, np.round(tot, 1).tolist()))))
+# tables phase split (stamps 41-43, thread 0 of workgroup 0): lane offsets + first chunk's loads
+# issued / coefficients staged / tables staged / barrier
+sub = np.zeros(4)
+for r in a:
+    t1, t41, t42, t43, t2 = r[1], r[41], r[42], r[43], r[2]
+    if min(t41, t42, t43) > 0:
+        sub += np.array([t41 - t1, t42 - t41, t43 - t42, t2 - t43]) / 100.0
+print("tables phase split (sum, us):", json.dumps(dict(zip(["lane_offs+chunk0_issue", "coeffs", "tables", "barrier"], np.round(sub, 1).tolist()))))
 # per-pass clocks of the first chunk (shader clock), grouped by pass kind
 kinds = {}
 for r in a:
