@@ -236,3 +236,16 @@ def test_slice_lanes_within_the_arena_budget():
     assert p4.query("lanes") == 4   # 1.1-GiB per-slice part: 4 lanes in the 6-GiB budget
     e2, p2 = _plan(config_task("C2"))
     assert p2.query("lanes") == 1   # one slice
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_lane_batched_boundary_gemm_and_lane_sum(cfg):
+    """With slice lanes the boundary GEMM (lane-local operands) is one batched launch per batch
+    (`lanes`), and since only the output permute reads its result the lanes' results are summed
+    before that permute runs once (`lane-sum`; tq_plan.cpp Op::lane_batch / lane_sum)."""
+    e, p = _plan(config_task(cfg))
+    d = p.describe().splitlines()
+    gemm = [l for l in d if " GEMM " in l]
+    assert len(gemm) == 1 and " lanes" in gemm[0] and "lane-sum" in gemm[0]
+    perm = [l for l in d if "PERMUTE result->out" in l]
+    assert len(perm) == 1 and "[slice]" in perm[0]
