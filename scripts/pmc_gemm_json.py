@@ -9,6 +9,9 @@ import collections, csv, json, sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_gemm_bf16_r02.json"
 kind = sys.argv[3] if len(sys.argv) > 3 else "bf16"
+# slices per launch (the plan's slice lanes: one batched launch per batch) and split-K count
+batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+splits = int(sys.argv[5]) if len(sys.argv) > 5 else 4
 F16 = kind == "f16"
 frag = "SplitF16" if F16 else "SplitBF16"
 pre = "pmcf" if F16 else "pmcx"
@@ -35,14 +38,14 @@ dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictRead
 avg_ns = sum(dur) / len(dur)
 M = N = 1024
 K = 65536
-n_mfma = (12 if F16 else 24) * (M // 32) * (N // 32) * (K // 16)  # 4M x (3 | 6) term products per tile-step
+n_mfma = batch * (12 if F16 else 24) * (M // 32) * (N // 32) * (K // 16)  # 4M x (3 | 6) term products per tile-step
 cyc_xcd = c1["GRBM_GUI_ACTIVE"] / 8
 res = {
     "config": "C4",
     "kernel": ("gemm_c64_kouter_split_kernel<TileH, SplitF16> (complex64 via 2-term f16 split of the "
                "power-of-two-scaled operands, 4M, " if F16 else
                "gemm_c64_kouter_split_kernel<TileX, SplitBF16> (complex64 via exact 3-term bf16 split, 4M, ")
-              + "M=N=1024, K=65536 per slice, block 128x128, split-K 4)",
+              + f"M=N=1024, K=65536 per slice, block 128x128, batch {batch} (slice lanes), split-K {splits})",
     "command": f"scripts/pmc_gemm_{kind}.sh (rocprofv3 --pmc ... --kernel-include-regex gemm_c64 -- python3 bench.py "
                "--no-cpu-baseline --no-c5 --steps 2 --warmup 1; FETCH_SIZE and WRITE_SIZE in separate passes; "
                "durations from a --kernel-trace pass)",
@@ -57,10 +60,12 @@ res = {
     "FETCH_SIZE_kB_per_launch": c2.get("FETCH_SIZE"),
     "WRITE_SIZE_kB_per_launch": c3.get("WRITE_SIZE"),
     "hbm_bytes_per_launch": (2 * c2.get("FETCH_SIZE", 0) + c3.get("WRITE_SIZE", 0)) * 1024,
-    "algorithmic_bytes_per_launch": (M * K + N * K) * 8 + 4 * M * N * 8,
+    "batch": batch,
+    "splits": splits,
+    "algorithmic_bytes_per_launch": batch * ((M * K + N * K) * 8 + splits * M * N * 8),
     "definition": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 XCDs * 256 CUs * 4 SIMDs); "
                   "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (kB, gfx950 FETCH correction); algorithmic bytes = "
-                  "A + B once + the 4 split-K partial slabs written",
+                  "batch x (A + B once + the split-K partial slabs, or C, written)",
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
