@@ -159,3 +159,63 @@ def contract(eq: str, *arrays: np.ndarray, path=None, exact: bool = True) -> np.
     (t, a), = live.values()
     t, a = _sum_out(t, a, set(rhs))
     return np.transpose(a, [t.index(c) for c in rhs]) if rhs else a.reshape(())
+
+
+def contract_sliced(eq: str, arrays: Sequence[np.ndarray], sliced: Sequence[str], path,
+                    slice_ids=None, exact: bool = True) -> np.ndarray:
+    """Sum over slices `slice_ids` (default: all) of contract(sliced_operands(eq, arrays, sliced,
+    s), path=path) -- the quantity a sliced execute call accumulates (tq_plan_execute; the
+    reference's partial contractions reduced by all_reduce(SUM), distributed_engine.py:1477-1497).
+    Path steps that read no sliced input are evaluated once and reused by every slice (the
+    result is the same as summing independent `contract` calls; only the work is shared)."""
+    terms, rhs = parse_equation(eq)
+    sl = set(sliced)
+    ext = {}
+    for t, a in zip(terms, arrays):
+        for c, e in zip(t, np.shape(a)):
+            ext[c] = e
+    n_sl = int(np.prod([ext[s] for s in sliced])) if sliced else 1
+    ids = range(n_sl) if slice_ids is None else slice_ids
+    conv = _exact if exact else (lambda a: a)
+    dep = {i: bool(set(t) & sl) for i, t in enumerate(terms)}
+    tlive = {i: t for i, t in enumerate(terms)}
+    nid = len(terms)
+    for i, j in path:   # dependence of every SSA value on a sliced input
+        dep[nid] = dep[i] or dep[j]
+        nid += 1
+    # slice-invariant SSA values, computed once (their terms hold no sliced symbol)
+    inv = {i: (t, conv(np.asarray(a))) for i, (t, a) in enumerate(zip(terms, arrays)) if not dep[i]}
+    live_t = dict(tlive)
+    nid = len(terms)
+    for i, j in path:
+        ti, tj = live_t.pop(i), live_t.pop(j)
+        if not dep[nid]:
+            keep = set(rhs)
+            for t in live_t.values():
+                keep |= set(t)
+            keep -= sl
+            inv[nid] = contract_pair(ti, inv[i][1], tj, inv[j][1], keep)
+            inv.pop(i)
+            inv.pop(j)
+        live_t[nid] = "".join(c for c in dict.fromkeys(ti + tj)) if dep[nid] else inv[nid][0]
+        nid += 1
+    total = None
+    for s in ids:
+        seq, sops = sliced_operands(eq, arrays, sliced, s)
+        sterms, _ = parse_equation(seq)
+        live = {i: (sterms[i], conv(sops[i])) for i in range(len(terms)) if dep[i]}
+        live.update({k: v for k, v in inv.items()})
+        nid = len(terms)
+        for i, j in path:
+            if dep[nid]:
+                (ti, a), (tj, b) = live.pop(i), live.pop(j)
+                keep = set(rhs)
+                for t, _ in live.values():
+                    keep |= set(t)
+                live[nid] = contract_pair(ti, a, tj, b, keep)
+            nid += 1
+        (t, a), = live.values()
+        t, a = _sum_out(t, a, set(rhs))
+        r = np.transpose(a, [t.index(c) for c in rhs]) if rhs else a.reshape(())
+        total = r.copy() if total is None else total + r
+    return total

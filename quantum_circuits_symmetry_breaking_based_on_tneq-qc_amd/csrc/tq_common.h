@@ -97,7 +97,7 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
                 void* workspace, size_t ws_bytes, hipStream_t stream,
                 const uint32_t* amax_a = nullptr, const uint32_t* amax_b = nullptr,
-                const struct GemmPresplit* presplit = nullptr);
+                const struct GemmPresplit* presplit = nullptr, int amax_bs_a = 0, int amax_bs_b = 0);
 // Operands stored as f16 terms by their producers (S2Op::split_sc; complex64 K-outer f16 path):
 // every element holds (h_re, h_im | l_re, l_im) of the value scaled by 2^sc.  The GEMM checks the
 // producers' true max words against the scales: outside the window (max * 2^sc in [2^0, 2^15))
@@ -118,7 +118,9 @@ bool gemm_presplit_enabled();
 int presplit_prep_launch(uint32_t* amax, int32_t* sc, int n, hipStream_t stream);
 // amax_a / amax_b (optional, complex64): float bits of max |re|, |im| over A / B, written by the
 // operands' producers (plan: the sweep ops that store them); the f16-split kernel then skips its
-// own max pre-pass over A and B
+// own max pre-pass over A and B.  amax_bs_a / amax_bs_b: word stride between batch entries (0: one
+// word for the whole batch; plan slice lanes: n_amax_slice, every lane scaled by its own max).
+// Without the words the pre-pass keeps one max per batch entry and operand.
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
 // apply a small operand along (at most two runs of) contracted modes (tq_apply.hip):
 //   C[o][n][m][i] = sum_{k1,k2} S[o][k1][m][k2][i] * G[k1*K2+k2][n]   (S, C, G contiguous)

@@ -131,7 +131,8 @@ struct GemmArgs {
 };
 
 constexpr int kThreads = 256;
-constexpr size_t kAmaxBytes = 256;  // f16 split: max-word block behind the split-K slabs
+// f16 split: max-word block behind the split-K slabs (two words per batch entry)
+inline size_t amax_bytes(int64_t batch) { return ((size_t)batch * 8 + 255) / 256 * 256; }
 
 // TQ_GEMM_FAST=0 disables the K-outer complex64 fast path (A/B timing of the two kernels)
 bool fast_disabled() {
@@ -424,6 +425,7 @@ struct FastArgs {
   const int32_t* sc_a;     // pre-split operands (SplitPre): the producers' scales, window flag
   const int32_t* sc_b;
   uint32_t* bad;
+  int amax_bs_a, amax_bs_b;  // max-word stride between batch entries (0: one word per operand)
 };
 
 template <int N>
@@ -819,21 +821,21 @@ __device__ __forceinline__ uint4 neg8(uint4 v) {
   return make_uint4(v.x ^ 0x80008000u, v.y ^ 0x80008000u, v.z ^ 0x80008000u, v.w ^ 0x80008000u);
 }
 
-// max |re|, |im| over the K x M (A) and K x N (B) operands of every batch, as float bits
-// atomically max-ed into amax[0] (A) / amax[1] (B) (zeroed before).  One wave per k-row,
-// 64 lanes x 16 B per load, four loads in flight; rows are M / 2 float4 (M % 128 == 0).
+// max |re|, |im| over the K x M (A) and K x N (B) operands of batch entry blockIdx.z, as float
+// bits atomically max-ed into amax[b] (A) / amax[batch + b] (B) (zeroed before).  One wave per
+// k-row, 64 lanes x 16 B per load, four loads in flight; rows are M / 2 float4 (M % 128 == 0).
 __global__ void __launch_bounds__(256) absmax_kouter_kernel(const float4* A, int64_t lda4, int64_t sA4,
                                                             const float4* B, int64_t ldb4, int64_t sB4,
                                                             int64_t K, int64_t w4A, int64_t w4B,
                                                             int64_t batch, uint32_t* amax) {
   const int op = blockIdx.y;
+  const int64_t b = blockIdx.z;
   const float4* base = op ? B : A;
   const int64_t ld = op ? ldb4 : lda4, s = op ? sB4 : sA4, w = op ? w4B : w4A;
   const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * 4, rows = K * batch;
+  const int64_t nw = (int64_t)gridDim.x * 4;
   float m = 0.f;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
-    const int64_t b = r / K, k = r - b * K;
+  for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < K; k += nw) {
     const float4* p = base + b * s + k * ld + lane;
     for (int64_t c = 0; c < w; c += 256) {
       float4 v[4];
@@ -851,7 +853,7 @@ __global__ void __launch_bounds__(256) absmax_kouter_kernel(const float4* A, int
   __syncthreads();
   if (threadIdx.x == 0) {
     m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    atomicMax(amax + op, __float_as_uint(m));
+    atomicMax(amax + op * batch + b, __float_as_uint(m));
   }
 }
 }  // namespace xbf
@@ -908,8 +910,9 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       return;
     }
   } else if constexpr (SP::SCALED) {
-    sca = scale_exp(*g.amax_a);
-    scb = scale_exp(*g.amax_b);
+    // every batch entry (slice lane) scaled by its own operand max
+    sca = scale_exp(g.amax_a[(int64_t)b * g.amax_bs_a]);
+    scb = scale_exp(g.amax_b[(int64_t)b * g.amax_bs_b]);
   }
 
   // staging registers, NSET sets (K-step mod NSET).  Threads 0 .. NT/2-1 stage A, the rest B
@@ -1522,7 +1525,7 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
                  const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB,
                  double beta, void* C, int64_t ldc, int64_t sC, void* W, size_t wsb,
                  hipStream_t stream, const uint32_t* amax_a, const uint32_t* amax_b,
-                 const GemmPresplit* ps) {
+                 const GemmPresplit* ps, int amax_bs_a, int amax_bs_b) {
   using C_ = Cfg<R, CPLX>;
   constexpr int EW = CPLX ? 2 : 1;
   constexpr int VE = 16 / (EW * (int)sizeof(R));
@@ -1553,21 +1556,25 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
         // the f16 split needs the two max words behind the split-K slabs
         const size_t slab = fs > 1 ? need : 0;
         const bool ext = amax_a != nullptr && amax_b != nullptr;
-        if (gemm_f16() && (ext || (W != nullptr && wsb >= slab + kAmaxBytes))) {
+        if (gemm_f16() && (ext || (W != nullptr && wsb >= slab + amax_bytes(batch) && batch <= 65535))) {
           if (ext) {
             f.amax_a = amax_a;
             f.amax_b = amax_b;
+            f.amax_bs_a = amax_bs_a;
+            f.amax_bs_b = amax_bs_b;
           } else {
+            // one max per batch entry and operand: every entry scaled by its own max
             uint32_t* amax = reinterpret_cast<uint32_t*>(static_cast<char*>(W) + slab);
-            TQ_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), stream));
-            const int64_t rows = K * batch;
-            const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1024));
-            hipLaunchKernelGGL(xbf::absmax_kouter_kernel, dim3(gx, 2), dim3(256), 0, stream,
+            TQ_HIP(hipMemsetAsync(amax, 0, 2 * batch * sizeof(uint32_t), stream));
+            const int64_t per = std::max<int64_t>(1, 1024 / batch);
+            const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((K + 3) / 4, per));
+            hipLaunchKernelGGL(xbf::absmax_kouter_kernel, dim3(gx, 2, (unsigned)batch), dim3(256), 0, stream,
                                (const float4*)A, lda / 2, sA / 2, (const float4*)B, ldb / 2, sB / 2, K,
                                M / 2, N / 2, batch, amax);
             TQ_HIP(hipGetLastError());
             f.amax_a = amax;
-            f.amax_b = amax + 1;
+            f.amax_b = amax + batch;
+            f.amax_bs_a = f.amax_bs_b = 1;
           }
           const int var = gemm_f16_var();
           if (ps) {
@@ -1729,19 +1736,19 @@ size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch)
   }
   const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   int s = choose_splits(tiles, K, (int)bk);
-  // the complex64 fast path also keeps the f16 split's two operand max words (kAmaxBytes)
+  // the complex64 fast path also keeps the f16 split's operand max words (amax_bytes)
   const int fs = dtype == TQ_C64 ? fast_c64_splits(1, 0, M, N, K, batch) : 0;
   s = std::max(s, fs);
   if (dtype == TQ_F64 || dtype == TQ_C128) s = std::max(s, fast_f64_splits(dtype, 1, 0, M, N, K, batch));
   const size_t slabs = s <= 1 ? 0 : (size_t)s * batch * M * N * dtype_size(dtype);
-  return fs > 0 ? slabs + kAmaxBytes : slabs;
+  return fs > 0 ? slabs + amax_bytes(batch) : slabs;
 }
 
 int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
                 const void* A, int64_t lda, int64_t strideA, const void* B, int64_t ldb,
                 int64_t strideB, double beta, void* C, int64_t ldc, int64_t strideC,
                 void* workspace, size_t ws_bytes, hipStream_t stream, const uint32_t* amax_a,
-                const uint32_t* amax_b, const GemmPresplit* presplit) {
+                const uint32_t* amax_b, const GemmPresplit* presplit, int amax_bs_a, int amax_bs_b) {
   TQ_CHECK_ARG(dtype_valid(dtype), "dtype");
   TQ_CHECK_ARG(presplit == nullptr || (dtype == TQ_C64 && amax_a && amax_b && presplit->sc_a &&
                                        presplit->sc_b && presplit->bad &&
@@ -1757,16 +1764,20 @@ int gemm_launch(int dtype, int transA, int transB, int64_t M, int64_t N, int64_t
   switch (dtype) {
     case TQ_F32:
       return launch_typed<float, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit,
+                                        amax_bs_a, amax_bs_b);
     case TQ_C64:
       return launch_typed<float, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
+                                       strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit,
+                                        amax_bs_a, amax_bs_b);
     case TQ_F64:
       return launch_typed<double, false>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
+                                         strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit,
+                                        amax_bs_a, amax_bs_b);
     case TQ_C128:
       return launch_typed<double, true>(transA, transB, M, N, K, batch, A, lda, strideA, B, ldb,
-                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit);
+                                        strideB, beta, C, ldc, strideC, workspace, ws_bytes, stream, amax_a, amax_b, presplit,
+                                        amax_bs_a, amax_bs_b);
   }
   return TQ_ERR_INVALID;
 }

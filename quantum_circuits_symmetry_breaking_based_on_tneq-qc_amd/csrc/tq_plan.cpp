@@ -306,7 +306,9 @@ class Compiler {
       tb += (b.size() + kAlign - 1) / kAlign * kAlign;
     }
     P_.amax_off = tb;
-    tb += ((size_t)(P_.n_amax_once + P_.n_amax_slice) * sizeof(uint32_t) + kAlign - 1) / kAlign * kAlign;
+    // per-slice words: one set per slice lane (every lane's operands scaled by their own max)
+    tb += ((size_t)(P_.n_amax_once + P_.n_amax_slice * std::max(1, P_.lanes)) * sizeof(uint32_t) + kAlign - 1) /
+          kAlign * kAlign;
     P_.sc_off = tb;
     tb += ((size_t)P_.n_amax_slice * sizeof(int32_t) + kAlign - 1) / kAlign * kAlign;
     P_.bad_off = tb;
@@ -2019,6 +2021,10 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       beta_out = (first && cur == 0) ? 0.0 : 1.0;
     };
     auto amax_word = [&](int w) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.amax_off) + w; };
+    // lane j's copy of max word w: per-slice words have one set per lane (the pre-split mode
+    // keeps one shared set: its scales are predicted per batch)
+    auto lane_amax_stride = [&](int w) { return (w >= P.n_amax_once && !P.run_mode) ? P.n_amax_slice : 0; };
+    auto amax_lane = [&](int w, int j) { return amax_word(w + j * lane_amax_stride(w)); };
     // scale word of per-slice max word w; window flag of slice q
     auto sc_word = [&](int w) { return reinterpret_cast<int32_t*>((char*)P.d_tables + P.sc_off) + (w - P.n_amax_once); };
     auto bad_word = [&](int64_t q) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.bad_off) + q; };
@@ -2046,14 +2052,16 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
                                op.b.kind == BUF_ARENA ? ls : 0, beta, ptr(op.c), op.ldc, ls,
                                (char*)P.d_arena + P.lane_ws_off, P.lane_ws_bytes, st,
                                op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
-                               op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, pre ? &ps : nullptr));
+                               op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, pre ? &ps : nullptr,
+                               op.amax_a >= 0 ? lane_amax_stride(op.amax_a) : 0,
+                               op.amax_b >= 0 ? lane_amax_stride(op.amax_b) : 0));
             break;
           }
           TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
                              op.lda, op.sA, ptr(op.b), op.ldb, op.sB, beta, ptr(op.c), op.ldc, op.sC,
                              op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, st,
-                             op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
-                             op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, pre ? &ps : nullptr));
+                             op.amax_a >= 0 ? amax_lane(op.amax_a, cur) : nullptr,
+                             op.amax_b >= 0 ? amax_lane(op.amax_b, cur) : nullptr, pre ? &ps : nullptr));
           break;
         }
         case OP_APPLY:
@@ -2183,7 +2191,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           blocks += o.nblocks;
           o.beta = op.writes_output ? beta_out : 0.0;
           o.use_beta = o.beta != 0.0;
-          o.amax = op.amax_word >= 0 ? amax_word(op.amax_word) : nullptr;
+          o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
           o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
         }
         TQ_TRY(sweep2_launch(P.dtype, L, stream));
@@ -2202,12 +2210,13 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
       for (auto& grp : P.sched_once) TQ_TRY(launch(grp));
     }
-    // per-slice max words: shared by the lanes of a batch (max-ed over all of them, an upper
-    // bound of every lane's operand)
+    // per-slice max words: one set per lane (pre-split mode: one set shared by the batch's
+    // lanes, max-ed over all of them -- an upper bound of every lane's operand)
     if (P.n_amax_slice && P.run_mode)   // scales from the previous slice's max, then max = 0
       TQ_TRY(presplit_prep_launch(amax_word(P.n_amax_once), sc_word(P.n_amax_once), P.n_amax_slice, stream));
     else if (P.n_amax_slice)
-      TQ_HIP(hipMemsetAsync(amax_word(P.n_amax_once), 0, P.n_amax_slice * sizeof(uint32_t), stream));
+      TQ_HIP(hipMemsetAsync(amax_word(P.n_amax_once), 0,
+                            (size_t)P.n_amax_slice * lane_sl.size() * sizeof(uint32_t), stream));
     bool lanes_summed = false;   // this batch's lanes were summed into lane 0 (Op::lane_sum)
     for (auto& grp : P.sched_slice) {
       const Op& op0 = P.ops[grp[0]];

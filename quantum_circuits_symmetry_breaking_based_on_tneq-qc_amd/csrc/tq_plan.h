@@ -113,7 +113,8 @@ struct Plan {
   std::vector<size_t> stab_off;
   size_t table_bytes = 0;
   // operand-max words behind the tables (zeroed per execute call: the first n_amax_once, written
-  // by slice-invariant producers; per slice: the next n_amax_slice)
+  // by slice-invariant producers; per slice batch: the next n_amax_slice x lanes, lane j's set at
+  // n_amax_once + j * n_amax_slice)
   size_t amax_off = 0;
   int n_amax_once = 0, n_amax_slice = 0;
   // pre-split GEMMs: scale words (one per per-slice max word), one window flag per slice, and

@@ -142,11 +142,19 @@ def main():
            "amplitudes_per_forward": int(np.prod(cands[0][0].out_shape)),
            "loss_after": [float(l.detach()) for l in losses]}
     if a.cpu_steps > 0:
-        torch.set_num_threads(min(16, os.cpu_count() or 1))
-        secs, n = cpu_step_sample(target.cpu().numpy(), cands, a.cpu_steps)
-        res["cpu_baseline"] = {"value": n / secs, "unit": "candidate-steps/s", "cores": torch.get_num_threads(),
-                               "kind": "port", "sample": f"{n} candidate-steps (torch CPU pairwise tensordot "
-                               "along the same path + autograd + oracle SGDG), complex128"}
+        # every host core and 16 (the box's CPU share per GPU): the faster counts
+        host = os.cpu_count() or 1
+        runs = []
+        for th in sorted({host, min(16, host)}, reverse=True):
+            torch.set_num_threads(th)
+            secs, n = cpu_step_sample(target.cpu().numpy(), cands, a.cpu_steps)
+            runs.append({"value": n / secs, "cores": torch.get_num_threads(), "sample": f"{n} candidate-steps"})
+        best = max(runs, key=lambda r: r["value"])
+        res["cpu_baseline"] = {"value": best["value"], "unit": "candidate-steps/s", "cores": best["cores"],
+                               "host_cpus": host, "by_threads": runs,
+                               "kind": "port", "sample": f"{best['sample']} (torch CPU pairwise tensordot "
+                               "along the same path + autograd + oracle SGDG), complex128, at every host "
+                               "core and at 16 threads; value = the faster"}
     print(json.dumps(res))
 
 

@@ -9,6 +9,14 @@ seconds and through size-independent properties where it does not.
   tq_plan_execute).  Normwise bounds (relative to max|amp|): complex64 2e-5, complex128 1e-12.
   Componentwise (the Gauss-3M imaginary part): every amplitude with
   |amp| >= 1e-2 max|amp| within 2e-3 relative, the normwise bound carried down to it.
+* C3 / C4 whole job EXACTLY as bench.py launches it (SlicedContraction at world 1 over the full
+  slice range: C4 4 slice lanes / C3 8, the lane-batched f16-split boundary GEMM with per-lane
+  operand-max words, lane_sum, lane-merged sweep launches, the captured hipGraph replayed)
+  against the oracle's sum over all slices (oracle.contract_ref.contract_sliced; the partial sums
+  the reference reduces at distributed_engine.py:1477-1497).
+* Lane skew: slices whose operands are 2^36 per cut leg larger than slice 0's, but whose
+  contribution is exactly zero, batched in the same lanes as slice 0: the result must be slice
+  0's amplitudes at full complex64 accuracy (a scale shared across lanes would flush them).
 * C3 / C4 whole job: sliced + hoisted execution equals the unsliced contraction (2e-5), every
   4-way rank shard of the slices sums to the full result, and 0 < sum |amp|^2 <= 1 (the
   amplitudes are a sub-block of a unitary circuit's |psi>).
@@ -74,6 +82,93 @@ def test_bench_config_slice_vs_oracle(dev, cfg, sid, dtype):
     big = np.abs(ref) >= 1e-2 * amax
     comp = (err[big] / np.abs(ref[big])).max()
     assert comp < TOL[dtype] * 100, (cfg, sid, dtype, comp)
+
+
+_ORACLE_FULL = {}
+
+
+def _oracle_full(cfg):
+    """Exact (complex128) sum over every slice of config `cfg`, cached per session."""
+    if cfg not in _ORACLE_FULL:
+        from oracle.contract_ref import contract_sliced
+        from tneq_qc_amd.circuits import config_task
+        t = config_task(cfg)
+        _ORACLE_FULL[cfg] = contract_sliced(t.eq, t.operands, t.sliced, t.path)
+    return _ORACLE_FULL[cfg]
+
+
+def _check(got, ref, tol, what):
+    amax = np.abs(ref).max()
+    err = np.abs(got - ref)
+    rel = err.max() / amax
+    assert rel < tol, (what, rel)
+    big = np.abs(ref) >= 1e-2 * amax
+    comp = (err[big] / np.abs(ref[big])).max()
+    assert comp < tol * 100, (what, comp)
+
+
+def _production_plan_checks(e, cfg, lanes):
+    import torch
+    plan = e.plan(torch.complex64)
+    assert plan.query("lanes") == lanes, plan.query("lanes")
+    d = plan.describe()
+    # the lane-batched boundary GEMM fed by its producers' max words, summed over lanes
+    assert " lanes" in d and "lane-sum" in d and "amax<-" in d, d
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg,lanes", [("C3", 8), ("C4", 4)])
+def test_bench_launch_vs_oracle(dev, cfg, lanes):
+    import torch
+    from tneq_qc_amd.circuits import config_task
+    from tneq_qc_amd.distributed import SlicedContraction
+    t = config_task(cfg)
+    e, ops = _expr_and_ops(t, dev, torch.complex64)
+    _production_plan_checks(e, cfg, lanes)
+    job = SlicedContraction(e)
+    out = torch.empty(e.out_shape, dtype=torch.complex64, device=dev)
+    plan = e.plan(torch.complex64)
+    g0 = plan.query("graph_launches")
+    res = []
+    for _ in range(3):   # first call captures the graph, the next ones replay it (as bench.py)
+        job(*ops, out=out)
+        res.append(out.cpu().numpy().copy())
+    assert plan.query("graph_launches") >= g0 + 2
+    ref = _oracle_full(cfg)
+    assert res[0].shape == ref.shape
+    for r in res:
+        _check(r, ref, TOL["complex64"], cfg)
+    assert np.array_equal(res[1], res[2])   # replays are deterministic
+
+
+@pytest.mark.parametrize("cfg,lanes", [("C3", 8), ("C4", 4)])
+def test_lane_skew_per_lane_scales(dev, cfg, lanes):
+    import torch
+    from tneq_qc_amd.circuits import config_task
+    t = config_task(cfg)
+    terms = t.eq.split("->")[0].split(",")
+    opsn = [o.copy() for o in t.operands]
+    n_var = int(np.log2(lanes))   # the last legs vary inside slice 0's lane batch
+    for q, s in enumerate(t.sliced):
+        holders = [i for i, x in enumerate(terms) if s in x]
+        assert len(holders) == 2, (s, holders)   # a cut bond: one core on each side
+        zi, bi = holders
+        ax_z, ax_b = terms[zi].index(s), terms[bi].index(s)
+        idx = [slice(None)] * opsn[zi].ndim
+        idx[ax_z] = slice(1, None)
+        opsn[zi][tuple(idx)] = 0            # every slice with this leg at 1 contributes 0 ...
+        if q < len(t.sliced) - n_var:
+            continue
+        idx = [slice(None)] * opsn[bi].ndim
+        idx[ax_b] = slice(1, None)
+        opsn[bi][tuple(idx)] *= 2.0 ** 36   # ... but its other operand is 2^36 larger
+    from tneq_qc_amd.expression import HipContractExpression
+    e = HipContractExpression(t.eq, *t.shapes, optimize=t.path, slices=t.sliced)
+    _production_plan_checks(e, cfg, lanes)
+    ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in opsn]
+    got = e(*ops).cpu().numpy()
+    assert np.isfinite(got).all()
+    _check(got, _oracle_slice(cfg, 0), TOL["complex64"], cfg)
 
 
 @pytest.mark.parametrize("cfg", ["C3", "C4"])

@@ -248,3 +248,25 @@ def test_gemm_c64_bench_shape(T, dev, c64_kernel):
     big = np.abs(ref) >= 1e-2 * np.abs(ref).max()
     comp = (np.abs(c[rows] - ref)[big] / np.abs(ref[big])).max()
     assert comp < TOL["complex64"] * 100, comp
+
+
+def test_gemm_c64_batched_entry_scales(T, dev, c64_kernel):
+    """A batched complex64 K-outer GEMM whose batch entries (the slice lanes of one plan launch)
+    differ in magnitude by up to 2^50: every entry keeps its own complex64 accuracy against
+    complex128 (the f16 split scales each batch entry by its own operand max; one max per launch
+    would flush the small entries' terms)."""
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(12)
+    M, N, K, B = 256, 256, 2048, 4
+    a = _rand(rng, (B, K, M), "complex128")
+    b = _rand(rng, (B, K, N), "complex128")
+    a[1] *= 2.0 ** -30
+    b[1] *= 2.0 ** -20
+    a[2] *= 2.0 ** 20
+    b[3] *= 2.0 ** -25
+    a, b = a.astype("complex64"), b.astype("complex64")
+    c = ops.gemm(_to(T, dev, a), _to(T, dev, b), True, False).cpu().numpy()
+    ref = np.matmul(np.swapaxes(a.astype("complex128"), 1, 2), b.astype("complex128"))
+    for i in range(B):
+        err = np.abs(c[i] - ref[i]).max() / np.abs(ref[i]).max()
+        assert err < TOL["complex64"], (i, err)
