@@ -305,6 +305,10 @@ class Compiler {
       P_.stab_off.push_back(tb);
       tb += (b.size() + kAlign - 1) / kAlign * kAlign;
     }
+    // constant operands in the tables (the compose ops' identity matrices): BufRef::index = blob
+    for (auto& op : P_.ops)
+      for (BufRef* r : {&op.a, &op.b})
+        if (r->kind == BUF_TABLE) r->off = (int64_t)P_.stab_off[r->index];
     P_.amax_off = tb;
     // per-slice words: one set per slice lane (every lane's operands scaled by their own max)
     tb += ((size_t)(P_.n_amax_once + P_.n_amax_slice * std::max(1, P_.lanes)) * sizeof(uint32_t) + kAlign - 1) /
@@ -965,6 +969,65 @@ class Compiler {
     }();
     return v != 0;
   }
+  static bool s2_dense_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_DENSE");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
+  // Dense form of a sweep chain (tq_sweepd.hip): complex64, a small input tile (tin <= 16), an
+  // output tile of <= 256, a big tensor (>= 2^20 output elements), and the six lowest column bits
+  // memory-fastest and contiguous in X and Y (a wave's 64 lanes = 64 consecutive elements).
+  bool s2_dense_layout(const Chain& c, const ChainShape& sh, const std::vector<int>& out_modes, S2Dense* dd) {
+    if (!s2_dense_enabled() || P_.dtype != TQ_C64 || !c.X0.contiguous()) return false;
+    // whole 32-output MFMA tiles (tq_sweepd.hip)
+    if (sh.tin_n < 2 || sh.tin_n > kS2DMaxTin || sh.tout_n < 32 || sh.tout_n > kS2DMaxTout || sh.tout_n % 32)
+      return false;
+    if (ilog2(sh.tin_n) < 0 || ilog2(sh.tout_n) < 0) return false;
+    std::map<int, int64_t> sx, sy;
+    {
+      auto cs = contig_strides(c.X0.ext);
+      for (size_t q = 0; q < c.X0.modes.size(); ++q) sx[c.X0.modes[q]] = cs[q];
+      std::vector<int64_t> ye;
+      for (int m : out_modes) ye.push_back(ext_[m]);
+      auto cy = contig_strides(ye);
+      for (size_t q = 0; q < out_modes.size(); ++q) sy[out_modes[q]] = cy[q];
+    }
+    std::vector<std::pair<int64_t, int64_t>> cb;
+    for (int m : sh.outer) {
+      const int nb = ilog2(ext_[m]);
+      if (nb < 0) return false;
+      for (int i = 0; i < nb; ++i) cb.push_back({sx[m] << i, sy.at(m) << i});
+    }
+    std::sort(cb.begin(), cb.end());
+    if (cb.size() < 6 || (int)cb.size() > kS2MaxColBits) return false;
+    for (int b = 0; b < 6; ++b)
+      if (cb[b].first != (int64_t(1) << b) || cb[b].second != (int64_t(1) << b)) return false;
+    const int64_t ncols = int64_t(1) << cb.size();
+    if (ncols * sh.tout_n < (int64_t(1) << 20)) return false;
+    dd->ncols = ncols;
+    dd->colbits = (int)cb.size();
+    dd->tin = (int)sh.tin_n;
+    dd->tout = (int)sh.tout_n;
+    for (size_t b = 0; b < cb.size(); ++b) { dd->w_in[b] = cb[b].first; dd->w_out[b] = cb[b].second; }
+    std::map<int, int64_t> dig;
+    for (int64_t t = 0; t < sh.tin_n; ++t) {
+      digits(t, sh.tin, dig);
+      int64_t o = 0;
+      for (int m : sh.tin) o += dig[m] * sx[m];
+      dd->in_off[t] = o;
+    }
+    for (int64_t t = 0; t < sh.tout_n; ++t) {
+      digits(t, sh.tout, dig);
+      int64_t o = 0;
+      for (int m : sh.tout) o += dig[m] * sy.at(m);
+      if (o >= (int64_t(1) << 31)) return false;   // the kernel stages them as int32
+      dd->out_off[t] = o;
+    }
+    return true;
+  }
+
   // GF(2) rank of a few small bit vectors
   static int gf2_rank(std::vector<int> v) {
     int r = 0;
@@ -1385,6 +1448,48 @@ class Compiler {
     return t;
   }
 
+  // one OP_SWEEP2 op: chain c (shape sh, layout d) from src (n0 elements) into tgt (nq)
+  void emit_s2(const Chain& c, const ChainShape& sh, const S2Desc& d, BufRef src, int64_t n0, BufRef tgt,
+               int64_t nq, bool direct, const char* what) {
+    Op op;
+    op.kind = OP_SWEEP2;
+    op.a = src;
+    op.c = tgt;
+    op.writes_output = direct;
+    op.step = c.gates.back().step;
+    op.tin = (int)sh.tin_n;
+    op.tout = (int)sh.tout_n;
+    op.ncols = d.ncols;
+    op.s2_nchunks = d.nchunks;
+    op.na = src.kind == BUF_TABLE ? 0 : n0;
+    op.nc = nq;
+    double flops = 0;
+    for (size_t j = 0; j < c.gates.size(); ++j) {
+      SweepGate sg;
+      sg.g = c.gates[j].Sm.buf;
+      sg.K = (int)c.gates[j].d.K;
+      sg.N = (int)c.gates[j].d.N;
+      sg.n = c.gates[j].Sm.numel();
+      op.sgates.push_back(sg);
+      flops += (double)d.ncols * count_of(sh.W[j]) * sg.K * (cplx_ ? 8.0 : 2.0);
+    }
+    std::vector<char> blob(sizeof(S2Desc));
+    std::memcpy(blob.data(), &d, sizeof(S2Desc));
+    op.stab = (int)P_.stabs.size();
+    P_.stabs.push_back(std::move(blob));
+    op.flops = flops;
+    op.bytes = (double)(n0 + nq) * P_.esz;
+    std::ostringstream o;
+    o << "step " << c.gates.front().step << ".." << op.step << " SWEEP2 " << what << "gates=" << c.gates.size()
+      << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " C=" << (1 << d.logC)
+      << " chunks=" << d.nchunks << (direct ? " ->OUT" : "") << " KxN=";
+    for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
+    o << " passes=" << d.npass;
+    if (d.epi) o << " epi";
+    op.note = o.str();
+    P_.ops.push_back(op);
+  }
+
   int flush_chain(bool final) {
     if (!chain_.active) return TQ_OK;
     Chain c = chain_;
@@ -1404,57 +1509,85 @@ class Compiler {
       const Live& B0 = g.d.a_big ? g.Sm : c.X0;
       TQ_TRY(emit_apply(g.step, g.d, final, A0, B0, res));
     } else if (shape_ok && sh0.s2) {
-      S2Desc d;
-      if (!s2_layout(c, sh0, c.out_modes, &d)) { set_error("internal: sweep2 layout"); return TQ_ERR_INVALID; }
       const int64_t n0 = c.X0.numel();
       const int64_t nq = n0 / sh0.tin_n * sh0.tout_n;
+      S2Dense dd;
+      const bool dense = s2_dense_layout(c, sh0, c.out_modes, &dd);
+      // dense: the chain composed on the identity first (a tiny sweep2 op into an arena matrix)
+      int64_t moff = -1;
+      BufRef mbuf;
+      if (dense) {
+        const int vm = 1 << 30;   // a column mode of its own: the basis vector index
+        ext_[vm] = sh0.tin_n;
+        Chain c2 = c;
+        c2.X0 = Live{};
+        c2.X0.modes = sh0.tin;
+        c2.X0.modes.push_back(vm);
+        for (int m : c2.X0.modes) c2.X0.ext.push_back(ext_[m]);
+        c2.X0.stride = contig_strides(c2.X0.ext);
+        std::vector<char> ident((size_t)(sh0.tin_n * sh0.tin_n) * P_.esz, 0);
+        for (int64_t k = 0; k < sh0.tin_n; ++k) {
+          const float one = 1.0f;
+          std::memcpy(ident.data() + (size_t)(k * sh0.tin_n + k) * P_.esz, &one, sizeof(float));
+        }
+        c2.X0.buf = BufRef{BUF_TABLE, (int64_t)P_.stabs.size(), 0, 0};
+        P_.stabs.push_back(std::move(ident));
+        std::vector<int> out2 = sh0.tout;
+        out2.push_back(vm);
+        ChainShape sh2;
+        S2Desc d2;
+        if (!chain_shape(c2, out2, sh2) || !sh2.s2 || !s2_layout(c2, sh2, out2, &d2)) {
+          ext_.erase(vm);
+          set_error("internal: sweep2 compose layout");
+          return TQ_ERR_INVALID;
+        }
+        ext_.erase(vm);
+        mbuf = new_buf(sh0.tin_n * sh0.tout_n, &moff);
+        emit_s2(c2, sh2, d2, c2.X0.buf, sh0.tin_n * sh0.tin_n, mbuf, sh0.tin_n * sh0.tout_n, false, "compose ");
+      }
       bool direct;
       int64_t roff;
       BufRef tgt = result_target(final, c.out_modes, nq, &direct, &roff);
-      Op op;
-      op.kind = OP_SWEEP2;
-      op.a = c.X0.buf;
-      op.c = tgt;
-      op.writes_output = direct;
-      op.step = c.gates.back().step;
-      op.tin = (int)sh0.tin_n;
-      op.tout = (int)sh0.tout_n;
-      op.ncols = d.ncols;
-      op.s2_nchunks = d.nchunks;
-      op.na = n0;
-      op.nc = nq;
-      double flops = 0;
-      for (size_t j = 0; j < c.gates.size(); ++j) {
-        SweepGate sg;
-        sg.g = c.gates[j].Sm.buf;
-        sg.K = (int)c.gates[j].d.K;
-        sg.N = (int)c.gates[j].d.N;
-        sg.n = c.gates[j].Sm.numel();
-        op.sgates.push_back(sg);
-        flops += (double)d.ncols * count_of(sh0.W[j]) * sg.K * (cplx_ ? 8.0 : 2.0);
+      if (dense) {
+        Op op;
+        op.kind = OP_SWEEP2;
+        op.s2_dense = true;
+        op.a = c.X0.buf;
+        op.b = mbuf;
+        op.c = tgt;
+        op.writes_output = direct;
+        op.step = c.gates.back().step;
+        op.tin = (int)sh0.tin_n;
+        op.tout = (int)sh0.tout_n;
+        op.ncols = dd.ncols;
+        op.na = n0;
+        op.nb = sh0.tin_n * sh0.tout_n;
+        op.nc = nq;
+        std::vector<char> blob(sizeof(S2Dense));
+        std::memcpy(blob.data(), &dd, sizeof(S2Dense));
+        op.stab = (int)P_.stabs.size();
+        P_.stabs.push_back(std::move(blob));
+        op.flops = (double)nq * sh0.tin_n * 8.0;
+        op.bytes = (double)(n0 + nq) * P_.esz;
+        std::ostringstream o;
+        o << "step " << c.gates.front().step << ".." << op.step << " SWEEP2 DENSE gates=" << c.gates.size()
+          << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << (direct ? " ->OUT" : "");
+        op.note = o.str();
+        P_.ops.push_back(op);
+        arenas_[region()].release(moff);
+      } else {
+        S2Desc d;
+        if (!s2_layout(c, sh0, c.out_modes, &d)) { set_error("internal: sweep2 layout"); return TQ_ERR_INVALID; }
+        emit_s2(c, sh0, d, c.X0.buf, n0, tgt, nq, direct, "");
       }
-      std::vector<char> blob(sizeof(S2Desc));
-      std::memcpy(blob.data(), &d, sizeof(S2Desc));
-      op.stab = (int)P_.stabs.size();
-      P_.stabs.push_back(std::move(blob));
-      op.flops = flops;
-      op.bytes = (double)(n0 + nq) * P_.esz;
-      std::ostringstream o;
-      o << "step " << c.gates.front().step << ".." << op.step << " SWEEP2 gates=" << c.gates.size()
-        << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " C=" << (1 << d.logC)
-        << " chunks=" << d.nchunks << (direct ? " ->OUT" : "") << " KxN=";
-      for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
-      o << " passes=" << d.npass;
-      if (d.epi) o << " epi";
-      op.note = o.str();
-      P_.ops.push_back(op);
       res.modes = c.out_modes;
       for (int m : c.out_modes) res.ext.push_back(ext_[m]);
       res.stride = contig_strides(res.ext);
       res.buf = tgt;
       res.owned = !direct;
       if (final && !direct)
-        TQ_TRY(emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, op.step, "result->out"));
+        TQ_TRY(emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, c.gates.back().step,
+                            "result->out"));
     } else {
       ChainShape sh = sh0;
       if (!shape_ok) { set_error("internal: chain shape"); return TQ_ERR_INVALID; }
@@ -2011,6 +2144,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
         case BUF_ARENA: return (char*)P.d_arena + P.lane_phys + (size_t)cur * P.lane_stride + b.off * esz;
         case BUF_PINNED: return (char*)P.d_arena + b.off * esz;
         case BUF_OUTPUT: return (char*)out + b.off * esz;
+        case BUF_TABLE: return (char*)P.d_tables + b.off;
       }
       return nullptr;
     };
@@ -2163,10 +2297,38 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       if (op0.kind == OP_SWEEP2) {
         // (lane, op) pairs of this level: every lane's ops when the level is merged across the
         // batch, else the current lane's; at most kS2MaxOps per launch
-        std::vector<std::pair<int, int>> items;
+        std::vector<std::pair<int, int>> items, dense;
         for (int j = 0; j < (lanes_merge ? (int)lane_sl.size() : 1); ++j)
-          for (int q : grp) items.push_back({lanes_merge ? j : cur, q});
+          for (int q : grp) (P.ops[q].s2_dense ? dense : items).push_back({lanes_merge ? j : cur, q});
         const int keep = cur;
+        // dense ops (tq_sweepd.hip): their own launches, one input tile size each
+        while (!dense.empty()) {
+          S2DLaunch L;
+          const int tin = P.ops[dense[0].second].tin;
+          std::vector<std::pair<int, int>> rest;
+          int blocks = 0;
+          for (auto& it : dense) {
+            const Op& op = P.ops[it.second];
+            if (op.tin != tin || L.nops == kS2MaxOps) { rest.push_back(it); continue; }
+            set_lane(it.first);
+            S2DOp& o = L.op[L.nops++];
+            o.desc = (const S2Dense*)((const char*)P.d_tables + P.stab_off[op.stab]);
+            o.X = ptr(op.a);
+            o.M = ptr(op.b);
+            o.Y = ptr(op.c);
+            o.tin = op.tin;
+            o.tout = op.tout;
+            o.block_begin = blocks;
+            o.nblocks = s2d_blocks(op.ncols);
+            blocks += o.nblocks;
+            o.beta = op.writes_output ? beta_out : 0.0;
+            o.use_beta = o.beta != 0.0;
+            o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
+            o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
+          }
+          TQ_TRY(sweepd_launch(P.dtype, L, stream));
+          dense.swap(rest);
+        }
         for (size_t i0 = 0; i0 < items.size(); i0 += kS2MaxOps) {
         S2Launch L;
         L.nops = (int)std::min<size_t>(kS2MaxOps, items.size() - i0);

@@ -64,6 +64,9 @@ struct Op {
   int load_colfast = 1, store_colfast = 1;
   // sweep2: descriptor blob = stabs[stab] (an S2Desc), launched with s2_blocks(s2_nchunks)
   int64_t s2_nchunks = 0;
+  // dense sweep (tq_sweepd.hip): stabs[stab] is an S2Dense, b = the tout x tin coefficient
+  // matrix written by the preceding compose op (a sweep2 op of the same chain on the identity)
+  bool s2_dense = false;
   // operand-max words (complex64 f16-split GEMM): a sweep2 op that produces a GEMM operand
   // max-es its stored values into word amax_word; the GEMM reads words amax_a / amax_b
   int amax_word = -1, amax_a = -1, amax_b = -1;

@@ -126,6 +126,45 @@ inline bool s2_lane_offsets_fit(const int64_t* ld_w, int nld, const int64_t* st_
 inline int s2_blocks(int64_t nchunks) { return (int)(nchunks < 512 ? nchunks : 512); }
 
 int sweep2_launch(int dtype, const S2Launch& L, hipStream_t stream);
+
+// ---- dense sweep (tq_sweepd.hip): an expanding chain with a small input tile (tin <= 16) on a
+// big tensor, Y[outer, r] = sum_k M[r][k] X[outer, k].  M (tout x tin, row-major: the tin
+// coefficients of output r contiguous) is the chain composed on the identity by a separate tiny
+// sweep2 op (the plan's "compose" op; the gates are device data).  No LDS tile and no gate
+// passes: a small-K complex GEMM on the f32 matrix cores per 32-column tile, the columns being
+// the memory-fastest bits of X and Y (coalesced loads and 256-B store segments).
+constexpr int kS2DMaxTin = 16;
+constexpr int kS2DMaxTout = 256;
+struct S2Dense {
+  int64_t ncols = 0;             // columns (outer index), a multiple of 64
+  int colbits = 0, tin = 0, tout = 0, pad = 0;
+  int64_t w_in[kS2MaxColBits] = {}, w_out[kS2MaxColBits] = {};  // column-bit weights (bits >= 6 used)
+  int64_t in_off[kS2DMaxTin] = {};     // memory offset of input tile element k
+  int64_t out_off[kS2DMaxTout] = {};   // memory offset of output tile element r
+};
+struct S2DOp {
+  const S2Dense* desc = nullptr;   // device copy (plan tables)
+  const void* X = nullptr;
+  void* Y = nullptr;
+  const void* M = nullptr;         // tout x tin coefficients
+  int block_begin = 0, nblocks = 0;
+  int tin = 0, tout = 0;           // host copies of the descriptor's (launch checks)
+  int use_beta = 0, pad = 0;
+  double beta = 0.0;
+  uint32_t* amax = nullptr;        // as S2Op::amax
+  const int32_t* split_sc = nullptr;  // as S2Op::split_sc
+};
+struct S2DLaunch {
+  int nops = 0, pad = 0;
+  S2DOp op[kS2MaxOps];
+};
+// blocks of a dense op (4 waves each, one 32-column tile per wave and iteration)
+inline int s2d_blocks(int64_t ncols) {
+  const int64_t tiles = ncols / 32;
+  const int64_t b = (tiles + 3) / 4;
+  return (int)(b < 256 ? b : 256);
+}
+int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream);
 int sweep2_timing(unsigned long long* out, int n);   // development instrumentation
 
 }  // namespace tq
