@@ -188,13 +188,16 @@ int tq_inverse_cdf_sample(int dtype, int64_t n_rows, int64_t grid_size, const vo
  * per parameter.  Parameter i is a rows[i] x cols[i] contiguous matrix (the parameter reshaped
  * to (prod of its leading half dims) x (rest), as SGDG.step views it) with a gradient of the
  * same shape and a momentum buffer.  flags[i]: TQ_SGDG_STIEFEL selects the Cayley branch (needs
- * rows <= cols <= 32; buffer cols x rows), otherwise the SGD branch with weight decay /
+ * rows <= cols <= TQ_SGDG_MAX_COLS; buffer cols x rows; matrices in LDS up to cols 32, on a
+ * stream-ordered global scratch above), otherwise the SGD branch with weight decay /
  * momentum / dampening / nesterov (buffer rows x cols; the gradient is updated in place by
  * the weight decay, as d_p.add_ does); TQ_SGDG_BUF_INIT = the buffer holds the previous
  * momentum (else it is initialised as the reference does: zeros / a copy of d_p);
  * TQ_SGDG_RETRACT = qr_retraction of the row-normalised parameter first (the reference draws
- * this with random.randint(1, 101) == 1 on the host).  Arithmetic in the parameter's precision. */
-enum { TQ_SGDG_STIEFEL = 1, TQ_SGDG_BUF_INIT = 2, TQ_SGDG_RETRACT = 4 };
+ * this with random.randint(1, 101) == 1 on the host).  Arithmetic in the parameter's precision.
+ * Every descriptor is checked before any parameter is touched: TQ_ERR_UNSUPPORTED (a Stiefel
+ * parameter outside the limits) leaves the whole group unchanged. */
+enum { TQ_SGDG_STIEFEL = 1, TQ_SGDG_BUF_INIT = 2, TQ_SGDG_RETRACT = 4, TQ_SGDG_MAX_COLS = 2048 };
 int tq_sgdg_step(int dtype, int n, void* const* params, void* const* grads, void* const* bufs,
                  const int32_t* rows, const int32_t* cols, const int32_t* flags, double lr,
                  double momentum, double dampening, double weight_decay, int nesterov,

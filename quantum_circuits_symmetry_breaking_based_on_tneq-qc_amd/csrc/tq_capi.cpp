@@ -324,6 +324,22 @@ int tq_sgdg_step(int dtype, int n, void* const* params, void* const* grads, void
   TQ_CHECK_ARG(n >= 0, "n");
   if (n == 0) return TQ_OK;
   TQ_CHECK_ARG(params && grads && bufs && rows && cols && flags, "null argument");
+  // every descriptor is checked before anything runs (no partly applied step)
+  size_t ws_total = 0;
+  for (int i = 0; i < n; ++i) {
+    const bool stf = flags[i] & tq::kSgdgStiefel;
+    TQ_CHECK_ARG(params[i] && grads[i] && rows[i] >= 1 && cols[i] >= 1, "bad parameter descriptor");
+    TQ_CHECK_ARG(bufs[i] || !(stf || momentum != 0.0), "missing momentum buffer");
+    if (stf && (rows[i] > cols[i] || cols[i] > tq::kSgdgMaxDimGlobal)) {
+      tq::set_error("sgdg: Stiefel parameters need rows <= cols <= " + std::to_string(tq::kSgdgMaxDimGlobal));
+      return TQ_ERR_UNSUPPORTED;
+    }
+    if (stf && cols[i] > tq::kSgdgMaxDim) ws_total += (tq::sgdg_ws_bytes(dtype, rows[i], cols[i]) + 255) / 256 * 256;
+  }
+  // large Stiefel parameters: one stream-ordered scratch for the call
+  char* ws = nullptr;
+  if (ws_total) TQ_HIP(hipMallocAsync((void**)&ws, ws_total, (hipStream_t)stream));
+  size_t ws_at = 0;
   for (int b = 0; b < n; b += tq::kSgdgMaxBatch) {
     tq::SgdgLaunch L{};
     L.n = std::min(n - b, tq::kSgdgMaxBatch);
@@ -333,11 +349,21 @@ int tq_sgdg_step(int dtype, int n, void* const* params, void* const* grads, void
     L.dampening = dampening;
     L.weight_decay = weight_decay;
     for (int i = 0; i < L.n; ++i) {
+      void* pw = nullptr;
+      if ((flags[b + i] & tq::kSgdgStiefel) && cols[b + i] > tq::kSgdgMaxDim) {
+        pw = ws + ws_at;
+        ws_at += (tq::sgdg_ws_bytes(dtype, rows[b + i], cols[b + i]) + 255) / 256 * 256;
+      }
       L.p[i] = tq::SgdgParam{params[b + i], grads[b + i], bufs[b + i], rows[b + i], cols[b + i],
-                             flags[b + i], 0};
+                             flags[b + i], 0, pw};
     }
-    TQ_TRY(tq::sgdg_launch(dtype, L, (hipStream_t)stream));
+    const int rc = tq::sgdg_launch(dtype, L, (hipStream_t)stream);
+    if (rc != TQ_OK) {
+      if (ws) (void)hipFreeAsync(ws, (hipStream_t)stream);
+      return rc;
+    }
   }
+  if (ws) TQ_HIP(hipFreeAsync(ws, (hipStream_t)stream));
   return TQ_OK;
   TQ_GUARD_END
 }

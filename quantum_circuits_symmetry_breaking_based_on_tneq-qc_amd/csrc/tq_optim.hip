@@ -4,7 +4,9 @@
 // SGDG.compute_Y (:66-74, the Cayley transform).  The symmetry-breaking training loop
 // (symmetry_breaking_quantum.py:216-230) runs this step on every core after every backward pass;
 // in the reference each core costs ~20 small torch launches (norms, 6 matmuls, an inverse), here the
-// whole group is one launch: one workgroup per parameter, every matrix in LDS.
+// whole group is one launch: one workgroup per parameter, every matrix in LDS (cols <= 32; larger
+// parameters -- a 1-D parameter is 1 x len, a core of bond dimension >= 3 has cols >= 9 ... -- run the
+// same code on a global-memory scratch, `GM`).
 //
 // Per parameter (X = the core viewed as row_dim x col_dim = p x n, row-normalised):
 //   Stiefel (p <= n):  V = momentum * buf - g^H;  MX = V X;  W^ = MX - 1/2 X^H X MX;
@@ -78,10 +80,12 @@ __device__ void mm(Cx<R>* C, const Cx<R>* A, int lda, const Cx<R>* B, int ldb, i
   }
 }
 
-template <typename T, typename R>
+template <typename T, typename R, bool GM>
 __global__ void __launch_bounds__(kThreads) sgdg_kernel(const SgdgLaunch L) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const SgdgParam P = L.p[blockIdx.x];
+  // GM launches hold only the large Stiefel parameters (and small ones: GM == false)
+  if (GM != (P.ws != nullptr)) return;
   const int p = P.rows, n = P.cols;
   const int64_t numel = (int64_t)p * n;
   const int tid = threadIdx.x;
@@ -112,7 +116,7 @@ __global__ void __launch_bounds__(kThreads) sgdg_kernel(const SgdgLaunch L) {
   }
   // ---- Stiefel branch: LDS layout (complex<R>): X p*n | V n*p | MX n*n | T1 p*n | W n*n |
   //      aug n*(n+p) | norms
-  Cx<R>* X = reinterpret_cast<Cx<R>*>(smem_raw);
+  Cx<R>* X = reinterpret_cast<Cx<R>*>(GM ? static_cast<char*>(P.ws) : smem_raw);
   Cx<R>* V = X + p * n;
   Cx<R>* MX = V + n * p;
   Cx<R>* T1 = MX + n * n;
@@ -230,24 +234,41 @@ __global__ void __launch_bounds__(kThreads) sgdg_kernel(const SgdgLaunch L) {
   }
 }
 
+// X p*n | V n*p | MX n*n | T1 p*n | W n*n | aug n*(n+p) | n reals
+template <typename R>
+size_t stiefel_bytes(int p, int n) {
+  const size_t cells = (size_t)p * n * 2 + (size_t)n * n * 2 + (size_t)n * p + (size_t)n * (n + p);
+  return cells * sizeof(Cx<R>) + (size_t)std::max(n, p) * sizeof(R) + 16;
+}
+
 template <typename T, typename R>
 int launch_t(const SgdgLaunch& L, hipStream_t stream) {
   int maxn = 1, maxp = 1;
-  for (int i = 0; i < L.n; ++i)
-    if (L.p[i].flags & kSgdgStiefel) {
+  bool small = false, large = false;
+  for (int i = 0; i < L.n; ++i) {
+    large = large || L.p[i].ws != nullptr;
+    small = small || L.p[i].ws == nullptr;
+    if ((L.p[i].flags & kSgdgStiefel) && !L.p[i].ws) {
       maxn = std::max(maxn, L.p[i].cols);
       maxp = std::max(maxp, L.p[i].rows);
     }
-  // X p*n | V n*p | MX n*n | T1 p*n | W n*n | aug n*(n+p) | n reals
-  const size_t cells = (size_t)maxp * maxn * 2 + (size_t)maxn * maxn * 2 + (size_t)maxn * maxp +
-                       (size_t)maxn * (maxn + maxp);
-  const size_t smem = cells * sizeof(Cx<R>) + (size_t)std::max(maxn, maxp) * sizeof(R) + 16;
-  hipLaunchKernelGGL((sgdg_kernel<T, R>), dim3(L.n), dim3(kThreads), smem, stream, L);
-  TQ_HIP(hipGetLastError());
+  }
+  if (small) {
+    hipLaunchKernelGGL((sgdg_kernel<T, R, false>), dim3(L.n), dim3(kThreads), stiefel_bytes<R>(maxp, maxn), stream, L);
+    TQ_HIP(hipGetLastError());
+  }
+  if (large) {
+    hipLaunchKernelGGL((sgdg_kernel<T, R, true>), dim3(L.n), dim3(kThreads), 16, stream, L);
+    TQ_HIP(hipGetLastError());
+  }
   return TQ_OK;
 }
 
 }  // namespace
+
+size_t sgdg_ws_bytes(int dtype, int rows, int cols) {
+  return (dtype == TQ_F64 || dtype == TQ_C128) ? stiefel_bytes<double>(rows, cols) : stiefel_bytes<float>(rows, cols);
+}
 
 int sgdg_launch(int dtype, const SgdgLaunch& L, hipStream_t stream) {
   if (L.n <= 0) return TQ_OK;
@@ -262,9 +283,15 @@ int sgdg_launch(int dtype, const SgdgLaunch& L, hipStream_t stream) {
       set_error("sgdg: bad parameter descriptor");
       return TQ_ERR_INVALID;
     }
-    if ((q.flags & kSgdgStiefel) && (q.rows > q.cols || q.cols > kSgdgMaxDim)) {
-      set_error("sgdg: Stiefel parameters need rows <= cols <= " + std::to_string(kSgdgMaxDim));
+    if ((q.flags & kSgdgStiefel) &&
+        (q.rows > q.cols || q.cols > kSgdgMaxDimGlobal || (q.cols > kSgdgMaxDim && !q.ws))) {
+      set_error("sgdg: Stiefel parameters need rows <= cols <= " + std::to_string(kSgdgMaxDimGlobal) +
+                " (a global scratch above " + std::to_string(kSgdgMaxDim) + ")");
       return TQ_ERR_UNSUPPORTED;
+    }
+    if (q.ws && !(q.flags & kSgdgStiefel)) {
+      set_error("sgdg: scratch given for a non-Stiefel parameter");
+      return TQ_ERR_INVALID;
     }
   }
   switch (dtype) {

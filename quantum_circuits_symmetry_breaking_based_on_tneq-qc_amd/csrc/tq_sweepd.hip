@@ -16,9 +16,9 @@
 //   * Gauss's 3M product (P1 = Mr Xr, P2 = Mi Xi, P3 = (Mr + Mi)(Xr + Xi); Dr = P1 - P2,
 //     Di = P3 - P1 - P2): 3 MFMAs per k-step and 32 x 32 tile; the sums Mr + Mi are an LDS plane
 //     of their own, Xr + Xi are formed once per column tile;
-//   * a wave owns a 32-column tile at a time, loads its tin inputs once and streams every
-//     32-output tile out of the accumulators (lane -> column, so a store instruction writes two
-//     256-B row segments).
+//   * a wave owns a 64-column group at a time, loads its tin inputs once and streams every
+//     32-output tile of both 32-column halves out of the accumulators (lane -> column: a store
+//     instruction writes two 256-B row segments; a row's two halves leave back to back).
 // A first version on the vector ALUs (coefficients by scalar loads) ran 1.9-4.7 TB/s: the
 // tout x tin coefficients (32 KiB at tin 16) stream through the scalar cache once per column
 // group.  Algorithmic bytes per op = (numel(X) + numel(Y)) * 8; 8 * tin flops per output.
@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
   f2v* __restrict__ Y = reinterpret_cast<f2v*>(op.Y);
   const int lane = threadIdx.x & 63, fr = lane & 31, fk = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ntiles = d->ncols >> 5;
+  const int64_t ngroups = d->ncols >> 6;
   const int64_t nw = (int64_t)op.nblocks * kWaves;
   const bool use_beta = op.use_beta;
   const float beta = (float)op.beta;
@@ -96,39 +96,46 @@ __global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
   int64_t io[KS];   // this lane's input offsets: element 2s + fk of the tile
 #pragma unroll
   for (int s = 0; s < KS; ++s) io[s] = d->in_off[2 * s + fk];
-  for (int64_t t = (int64_t)((int)blockIdx.x - op.block_begin) * kWaves + wave; t < ntiles; t += nw) {
-    // column tile t: columns 32t .. 32t+31 (bits 0..4 = lane, bit 5 = t & 1, bits >= 6 uniform)
-    const int64_t g = t >> 1;
+  // a wave owns a 64-column group (two 32-column MFMA tiles, h = 0 / 1): every 32-output tile
+  // is computed and stored for both halves back to back, so the two 256-B halves of each
+  // 512-B output row segment leave within a few hundred cycles of each other
+  for (int64_t g = (int64_t)((int)blockIdx.x - op.block_begin) * kWaves + wave; g < ngroups; g += nw) {
     int64_t bi = 0, bo = 0;
     for (int b = 6; b < colbits; ++b)
       if ((g >> (b - 6)) & 1) { bi += d->w_in[b]; bo += d->w_out[b]; }
-    const int cl = (int)(t & 1) * 32 + fr;
-    float xr[KS], xi[KS], xs[KS];
+    float xr[2][KS], xi[2][KS], xs[2][KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const f2v v = X[bi + io[s] + cl];
-      xr[s] = v.x;
-      xi[s] = v.y;
-      xs[s] = v.x + v.y;
-    }
-    for (int rt = 0; rt < tout; rt += 32) {
-      f32x16 p1 = {}, p2 = {}, p3 = {};
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int a = (2 * s + fk) * tout + rt + fr;
-        p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[0][a], xr[s], p1, 0, 0, 0);
-        p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[1][a], xi[s], p2, 0, 0, 0);
-        p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[2][a], xs[s], p3, 0, 0, 0);
+        const f2v v = X[bi + io[s] + h * 32 + fr];
+        xr[h][s] = v.x;
+        xi[h][s] = v.y;
+        xs[h][s] = v.x + v.y;
       }
-      // accumulator e of a lane: output row rt + (e & 3) + 8 (e >> 2) + 4 fk, column cl
+    for (int rt = 0; rt < tout; rt += 32) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int r = rt + (e & 3) + 8 * (e >> 2) + 4 * fk;
-        f2v v = {p1[e] - p2[e], p3[e] - p1[e] - p2[e]};
-        f2v* p = Y + (bo + ooff[r] + cl);
-        if (use_beta) v += *p * beta;
-        if (track) vmax = fmaxf(vmax, fmaxf(fabsf(v.x), fabsf(v.y)));
-        *p = split ? f16_terms(v, sc) : v;
+      for (int h = 0; h < 2; ++h) {
+        f32x16 p1 = {}, p2 = {}, p3 = {};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int a = (2 * s + fk) * tout + rt + fr;
+          p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[0][a], xr[h][s], p1, 0, 0, 0);
+          p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[1][a], xi[h][s], p2, 0, 0, 0);
+          p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[2][a], xs[h][s], p3, 0, 0, 0);
+        }
+        // accumulator e of a lane: output row rt + (e & 3) + 8 (e >> 2) + 4 fk, column h*32 + fr
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = rt + (e & 3) + 8 * (e >> 2) + 4 * fk;
+          f2v v = {p1[e] - p2[e], p3[e] - p1[e] - p2[e]};
+          f2v* p = Y + (bo + ooff[r] + h * 32 + fr);
+          if (use_beta) v += *p * beta;
+          if (track) vmax = fmaxf(vmax, fmaxf(fabsf(v.x), fabsf(v.y)));
+          *p = split ? f16_terms(v, sc) : v;
+          // keeps the 16 store addresses from being formed (and held) all at once
+          if ((e & 3) == 3) asm volatile("" ::: "memory");
+        }
       }
     }
   }

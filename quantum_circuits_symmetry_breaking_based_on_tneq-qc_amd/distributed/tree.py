@@ -131,15 +131,8 @@ class TreeContraction:
             self.stages.append(row)
         if self.world == 1:
             self.local[0] = out
-        # process groups of every stage (created by every rank, same order)
-        self._pg = {}
-        if self.world > 1 and dist.is_initialized():
-            for row in self.stages:
-                for st in row:
-                    if st is None:
-                        continue
-                    ranks = [self.granks[r] for r in range(st.g, min(st.g + 2 ** st.s, self.world))]
-                    self._pg[(st.s, st.g)] = dist.new_group(ranks)
+        # stage exchanges are point-to-point within `group` (no per-stage process groups: they
+        # would have to be created by every rank of the world, and `group` may be a subgroup)
         self._exprs = {}
 
     # -- execution -----------------------------------------------------------------------
@@ -180,23 +173,74 @@ class TreeContraction:
                 if not (st.g <= r < st.g + G):
                     continue
                 pos = r - st.g
-                pg = self._pg.get((st.s, st.g))
                 H = 2 ** (st.s - 1)
+                members = [self.granks[q] for q in range(st.g, st.g + G)]
                 left = cur if pos < H else torch.empty(st.shapes[0], dtype=cur.dtype, device=cur.device)
                 right = cur if pos >= H else torch.empty(st.shapes[1], dtype=cur.dtype, device=cur.device)
                 left, right = left.contiguous(), right.contiguous()
-                if pg is not None:
-                    _bcast(left, self.granks[st.g], pg)
-                    _bcast(right, self.granks[st.g + H], pg)
+                # the left block (leader st.g) and the right block (leader st.g + H) to every
+                # member (the reference's SendRecvGrad exchange, distributed_engine.py:1697-1766)
+                _p2p_bcast([left, right], [members[0], members[H]], members, self.granks[r], self.group)
                 part = self._contract(("stage", st.s, st.g), st.eq, st.shapes, [left, right],
-                                      st.slice_syms, (pos, None, G))
-                if pg is not None:
-                    v = torch.view_as_real(part) if part.is_complex() else part
-                    dist.all_reduce(v, op=dist.ReduceOp.SUM, group=pg)
+                                      st.slice_syms, (pos, None, G)).contiguous()
+                # sum of the members' K-shard partials (allreduce_grad.py:13-60), in member order
+                _p2p_allreduce(part, members, self.granks[r], self.group)
                 cur = part
         return cur
 
 
-def _bcast(t: torch.Tensor, src: int, group):
-    v = torch.view_as_real(t) if t.is_complex() else t
-    dist.broadcast(v, src=src, group=group)
+def _view(t: torch.Tensor) -> torch.Tensor:
+    return torch.view_as_real(t) if t.is_complex() else t
+
+
+def _staged(t: torch.Tensor, group) -> bool:
+    """gloo moves host memory only: device tensors go through a host copy there (RCCL takes
+    them directly)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _p2p_bcast(tensors, srcs, members, me, group):
+    """tensors[i] from global rank srcs[i] to every other member: receives posted first, then
+    sends, then one wait (no ordering deadlock)."""
+    reqs, back = [], []
+    for t, src in zip(tensors, srcs):
+        if me != src:
+            buf = torch.empty(t.shape, dtype=t.dtype) if _staged(t, group) else t
+            reqs.append(dist.irecv(_view(buf), src=src, group=group))
+            if buf is not t:
+                back.append((buf, t))
+    for t, src in zip(tensors, srcs):
+        if me == src:
+            buf = t.cpu() if _staged(t, group) else t
+            for m in members:
+                if m != src:
+                    reqs.append(dist.isend(_view(buf), dst=m, group=group))
+    for q in reqs:
+        q.wait()
+    for buf, t in back:
+        t.copy_(buf)
+
+
+def _p2p_allreduce(t: torch.Tensor, members, me, group):
+    """In-place SUM over the members: the leader adds the partials in member order and sends
+    the total back (deterministic; a stage group holds at most 2^s ranks)."""
+    if len(members) == 1:
+        return
+    lead = members[0]
+    host = t.cpu() if _staged(t, group) else t
+    v = _view(host)
+    if me == lead:
+        bufs = [torch.empty_like(v) for _ in members[1:]]
+        reqs = [dist.irecv(b, src=m, group=group) for b, m in zip(bufs, members[1:])]
+        for q in reqs:
+            q.wait()
+        for b in bufs:
+            v += b
+        reqs = [dist.isend(v, dst=m, group=group) for m in members[1:]]
+    else:
+        dist.isend(v, dst=lead, group=group).wait()
+        reqs = [dist.irecv(v, src=lead, group=group)]
+    for q in reqs:
+        q.wait()
+    if host is not t:
+        t.copy_(host)

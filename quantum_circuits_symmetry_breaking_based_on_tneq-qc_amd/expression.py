@@ -250,9 +250,10 @@ class _ReverseTree:
     full-network contraction per operand.
 
     Runtime (_TreeRuntime): intermediates and gradients live in static buffers per (dtype,
-    device); the step plans launch eagerly and, once an input-pointer set repeats (a training
-    loop updating its parameters in place), the whole forward / backward launch sequence is
-    captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed."""
+    device, stream) -- two streams running one expression concurrently do not share them; the
+    step plans launch eagerly and, once an input-pointer set repeats (a training loop updating
+    its parameters in place), the whole forward / backward launch sequence is captured once into
+    a hipGraph (torch.cuda.CUDAGraph) and replayed."""
 
     def __init__(self, expr: "HipContractExpression"):
         net = expr.net
@@ -292,7 +293,7 @@ class _ReverseTree:
         self._rt: Dict[tuple, "_TreeRuntime"] = {}
 
     def runtime(self, dtype, device) -> "_TreeRuntime":
-        key = (dtype, device.index)
+        key = (dtype, device.index, torch.cuda.current_stream(device).cuda_stream)
         rt = self._rt.get(key)
         if rt is None:
             rt = self._rt[key] = _TreeRuntime(self, dtype, device)
@@ -301,9 +302,11 @@ class _ReverseTree:
 
 class _TreeRuntime:
     _MAX_GRAPHS = 4
+    _MAX_SEEN = 64     # pointer sets remembered for the capture-on-repeat rule
 
     def __init__(self, tree: _ReverseTree, dtype, device):
         self.tree, self.dtype, self.dev = tree, dtype, device
+        self.stream = torch.cuda.current_stream(device).cuda_stream   # the stream it is keyed on
         t = tree
         shape = lambda n: tuple(t.ext[m] for m in t.modes[n])
         with torch.cuda.device(device):
@@ -370,6 +373,8 @@ class _TreeRuntime:
             g.replay()
             return
         n = self.seen.get(key, 0) + 1
+        if n == 1 and len(self.seen) >= self._MAX_SEEN:   # bounded: forget the oldest pointer set
+            self.seen.pop(next(iter(self.seen)))
         self.seen[key] = n
         if n < 2 or _graphs_off():
             fn()
@@ -443,7 +448,10 @@ class _HipContractFn(torch.autograd.Function):
             rt = rev.runtime(dt, dev)
             with torch.cuda.device(dev):
                 out = rt.forward(ins).clone()
-        ctx.ins, ctx.rt, ctx.gen = ins, rt, rt.gen
+        # saved through autograd: a second backward (retain_graph=True) finds them again, and an
+        # in-place change of an input between forward and backward raises (version counter)
+        ctx.save_for_backward(*ins)
+        ctx.rt, ctx.gen = rt, rt.gen
         return out
 
     @staticmethod
@@ -458,12 +466,13 @@ class _HipContractFn(torch.autograd.Function):
             for k in bcast:
                 g = g.unsqueeze(k)
             return (None, g.expand(t.shape).to(device=t.device, dtype=t.dtype))
-        rt, ins = ctx.rt, ctx.ins
+        rt, ins = ctx.rt, list(ctx.saved_tensors)
+        # (autograd runs this on the forward's stream: the runtime's own)
         with torch.cuda.device(rt.dev):
             if rt.gen != ctx.gen:        # another forward reused the static buffers: recompute
                 rt.forward(ins)
+                ctx.gen = rt.gen
             g = rt.backward(ins, grad_out, needs)
-        ctx.ins = None
         out = [None]
         for gi, (dt, dev, shape), nd in zip(g, ctx.in_meta, needs):
             if not nd:

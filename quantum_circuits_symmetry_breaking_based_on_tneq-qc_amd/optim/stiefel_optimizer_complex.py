@@ -10,8 +10,12 @@ exactly where the reference does (a 1 triggers qr_retraction of the row-normalis
 parameter); every other parameter takes the SGD branch (weight decay / momentum / dampening /
 nesterov, the gradient updated in place by the weight decay as d_p.add_ does).
 The arithmetic of a whole group is ONE native launch (tq_sgdg_step: one workgroup per
-parameter, every matrix LDS-resident, the Cayley solve by Gauss-Jordan) instead of ~20 small
-torch launches per parameter.  Parameters must live on the HIP device; there is no CPU path.
+parameter, every matrix LDS-resident up to 32 columns and on a global scratch above -- 1-D
+parameters are 1 x len, cores of bond dimension >= 3 have cols >= 9 --, the Cayley solve by
+Gauss-Jordan) instead of ~20 small torch launches per parameter.  Parameters must live on the
+HIP device; there is no CPU path.  Every parameter of every group is checked (device, dtype,
+layout, Stiefel shape limit) before any random draw, state change or launch, so an unsupported
+parameter raises with the optimizer and the parameters untouched.
 """
 from __future__ import annotations
 
@@ -25,6 +29,7 @@ from .. import _lib
 
 _DT = {torch.float32: _lib.TQ_F32, torch.float64: _lib.TQ_F64,
        torch.complex64: _lib.TQ_C64, torch.complex128: _lib.TQ_C128}
+MAX_STIEFEL_COLS = 2048   # TQ_SGDG_MAX_COLS (include/tneqhip.h)
 
 
 def _view_dims(size):
@@ -60,9 +65,8 @@ class SGDG(Optimizer):
             with torch.enable_grad():
                 loss = closure()
         L = _lib.lib()
+        # every parameter is checked before anything is drawn, created or launched
         for group in self.param_groups:
-            momentum, stiefel = group["momentum"], group["stiefel"]
-            batches = {}   # (dtype, device) -> list of descriptors, in parameter order
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -70,9 +74,19 @@ class SGDG(Optimizer):
                     raise ValueError("SGDG (HIP) needs parameters on the HIP device")
                 if p.dtype not in _DT:
                     raise ValueError(f"SGDG (HIP): unsupported dtype {p.dtype}")
-                rows, cols = _view_dims(p.size())
                 if not p.is_contiguous() or not p.grad.is_contiguous():
                     raise ValueError("SGDG (HIP) needs contiguous parameters and gradients")
+                rows, cols = _view_dims(p.size())
+                if group["stiefel"] and rows <= cols and cols > MAX_STIEFEL_COLS:
+                    raise ValueError(f"SGDG (HIP): Stiefel parameter {tuple(p.size())} has {cols} columns "
+                                     f"(at most {MAX_STIEFEL_COLS})")
+        for group in self.param_groups:
+            momentum, stiefel = group["momentum"], group["stiefel"]
+            batches = {}   # (dtype, device) -> list of descriptors, in parameter order
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                rows, cols = _view_dims(p.size())
                 st = self.state[p]
                 flags = 0
                 if stiefel and rows <= cols:

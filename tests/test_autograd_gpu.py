@@ -117,3 +117,58 @@ def test_repeated_steps_hit_the_captured_graph_and_stay_exact(dev):
     r1 = torch.autograd.grad(torch.einsum(eq, *c1).abs().square().sum(), c1)
     for a, b in zip(g1, r1):
         assert torch.allclose(a.cpu(), b, atol=1e-10)
+
+
+def test_retain_graph_second_backward_and_inplace_guard(dev):
+    """a second backward with retain_graph=True gives the same gradients; an in-place
+    change of an input between forward and backward raises (autograd's version counter), as
+    torch.einsum's own backward would."""
+    import torch
+    from tneq_qc_amd.expression import HipContractExpression
+    rng = np.random.default_rng(3)
+    shapes = [(3, 4), (4, 5), (5, 3)]
+    ts = [torch.tensor(rng.standard_normal(s) + 1j * rng.standard_normal(s), device=dev, requires_grad=True)
+          for s in shapes]
+    e = HipContractExpression("ab,bc,ca->", *shapes)
+    out = e(*ts)
+    loss = (out * (2 - 1j)).real
+    g1 = torch.autograd.grad(loss, ts, retain_graph=True)
+    g2 = torch.autograd.grad(loss, ts)
+    for a, b in zip(g1, g2):
+        assert torch.allclose(a, b, atol=1e-12)
+    x = [t.detach().clone().requires_grad_(True) for t in ts]
+    y = [t * 1 for t in x]   # non-leaf inputs that can be modified in place
+    out = e(*y)
+    with torch.no_grad():
+        y[1].mul_(2.0)
+    with pytest.raises(RuntimeError):
+        out.real.backward()
+
+
+def test_one_expression_on_two_streams(dev):
+    """one expression differentiated concurrently on two streams keeps per-stream
+    static buffers: both gradients equal the single-stream ones."""
+    import torch
+    from tneq_qc_amd.expression import HipContractExpression
+    rng = np.random.default_rng(4)
+    shapes = [(8, 8, 4), (4, 8), (8, 8)]
+    e = HipContractExpression("abc,cd,db->a", *shapes)
+    sets = [[torch.tensor(rng.standard_normal(s) + 1j * rng.standard_normal(s), device=dev, requires_grad=True)
+             for s in shapes] for _ in range(2)]
+    ref = []
+    for ts in sets:
+        ref.append(torch.autograd.grad(e(*ts).abs().sum(), ts))
+    st = [torch.cuda.Stream(dev) for _ in range(2)]
+    got = [None, None]
+    for _ in range(3):   # the third round replays captured graphs
+        cur = torch.cuda.current_stream(dev)
+        for k in range(2):
+            st[k].wait_stream(cur)
+            with torch.cuda.stream(st[k]):
+                got[k] = torch.autograd.grad(e(*sets[k]).abs().sum(), sets[k])
+        for k in range(2):
+            cur.wait_stream(st[k])
+        torch.cuda.synchronize(dev)
+        for k in range(2):
+            for a, b in zip(got[k], ref[k]):
+                assert torch.allclose(a, b, atol=1e-11)

@@ -221,3 +221,42 @@ def test_fused_sweep_chains_random(dev, dtype, seed):
     acc = torch.from_numpy(np.ascontiguousarray(ref)).to(dev, getattr(torch, dtype))
     e(*ts, out=acc, accumulate=True)
     assert _err(acc.cpu().numpy(), 2 * ref) < tol
+
+
+@pytest.mark.parametrize("dtype", ["complex128", "complex64"])
+def test_engine_contract_with_vector_inputs(dev, dtype):
+    """Engine.contract_with_vector_inputs (engine.py:285-315), the reference's amplitude-vector
+    API, on the 'hip' backend: psi of an 8-qubit brick wall on random product-state inputs
+    == the oracle's vector-inputs equation (oracle.qctn_ref, einsum_strategy.py:258-318)
+    contracted exactly; the expression is cached on the QCTN under the reference's attribute
+    and reused; core-only / single-input / two-QCTN entry points too."""
+    import torch
+    from oracle import qctn_ref
+    from tneq_qc_amd.backends import BackendFactory
+    from tneq_qc_amd.circuits import BrickWall
+    from tneq_qc_amd.core import Engine, QCTN
+    bw = BrickWall(8, 4, 2)
+    be = BackendFactory.create_backend("hip", device="cuda", dtype=dtype)
+    q = QCTN(bw.graph, backend=be)
+    q.set_cores({c: torch.from_numpy(bw.cores[c]) for c in q.cores})
+    eng = Engine(backend=be)
+    rng = np.random.default_rng(9)
+    vecs = [(rng.standard_normal(2) + 1j * rng.standard_normal(2)) for _ in range(8)]
+    psi = eng.contract_with_vector_inputs(q, vecs).cpu().numpy()
+    qr = qctn_ref.QCTNRef(bw.graph)
+    eq, _ = qctn_ref.build_with_vector_inputs_expression(qr, [(2,)] * 8)
+    ref = ref_contract(eq, *vecs, *[bw.cores[c] for c in qr.cores])
+    assert psi.shape == ref.shape and _err(psi, ref) < TOL[dtype]
+    key = f"_contract_expr_vector_inputs_{tuple([torch.Size([2])] * 8)}"
+    assert hasattr(q, key)
+    expr = getattr(q, key)
+    psi2 = eng.contract_with_vector_inputs(q, vecs).cpu().numpy()
+    assert getattr(q, key) is expr and _err(psi2, ref) < TOL[dtype]
+    # core-only (the 2^16-amplitude unitary of the 8 legs) and two-QCTN overlap
+    u = eng.contract_core_only(q).cpu().numpy()
+    eq_c, _ = qctn_ref.build_core_only_expression(qr)
+    assert _err(u, ref_contract(eq_c, *[bw.cores[c] for c in qr.cores])) < TOL[dtype]
+    ov = eng.contract_with_qctn(q, q).cpu().numpy()
+    eq_q, _ = qctn_ref.build_with_qctn_expression(qr, qr)
+    cores = [bw.cores[c] for c in qr.cores]
+    assert _err(ov, ref_contract(eq_q, *cores, *cores)) < TOL[dtype]

@@ -93,3 +93,60 @@ def test_sgdg_workload_loop_keeps_cores_unitary_and_fits(dev):
     for p in params:
         u = p.detach().reshape(4, 4)
         assert torch.allclose(u @ u.conj().T, eye, atol=1e-10)
+
+
+@pytest.mark.parametrize("dtype", ["complex128", "complex64", "float64"])
+def test_sgdg_large_and_1d_stiefel_params_match_oracle(dev, dtype):
+    """Stiefel parameters beyond the LDS-resident size: a 1-D parameter (1 x 100), a
+    bond-dimension-3 core (3,3,3,3) -> 9 x 9 (LDS), a (4,4,4,4) core -> 16 x 16, a (2,40) -> 2 x 40
+    and a (3, 64) -> 3 x 64 parameter (global scratch), with momentum and a forced qr_retraction,
+    against the oracle over 3 steps."""
+    import torch
+    from oracle.optim_ref import sgdg_step
+    from tneq_qc_amd.optim import SGDG
+    cplx = dtype.startswith("complex")
+    rng = np.random.default_rng(11)
+    shapes = [(100,), (3, 3, 3, 3), (4, 4, 4, 4), (2, 40), (3, 64)]
+    ref = []
+    for s in shapes:
+        a = rng.standard_normal(s) + (1j * rng.standard_normal(s) if cplx else 0)
+        ref.append(a.astype(dtype))
+    params = [torch.nn.Parameter(torch.from_numpy(p.copy()).to(dev)) for p in ref]
+    hp = dict(lr=0.05, momentum=0.9, stiefel=True)
+    opt = SGDG(params, **hp)
+    state = {}
+    seeds = [next(s for s in range(10000) if (random.seed(s), random.randint(1, 101))[1] == 1), 5, 6]
+    for step, seed in enumerate(seeds):
+        grads = [(rng.standard_normal(p.shape) + (1j * rng.standard_normal(p.shape) if cplx else 0)).astype(dtype)
+                 for p in ref]
+        for p, g in zip(params, grads):
+            p.grad = torch.from_numpy(g.copy()).to(dev)
+        random.seed(seed)
+        opt.step()
+        random.seed(seed)
+        sgdg_step(ref, [g.copy() for g in grads], state, **hp)
+        torch.cuda.synchronize()
+        for i, (p, r) in enumerate(zip(params, ref)):
+            got = p.detach().cpu().numpy()
+            err = np.abs(got - r).max() / max(np.abs(r).max(), 1e-30)
+            assert err < TOL[dtype] * 10, (step, shapes[i], err)
+
+
+def test_sgdg_rejects_oversized_before_touching_anything(dev):
+    """A Stiefel parameter over the column limit raises before any random draw, momentum buffer
+    or launch: the other parameters, the optimizer state and `random`'s stream are unchanged."""
+    import torch
+    from tneq_qc_amd.optim import SGDG
+    from tneq_qc_amd.optim.stiefel_optimizer_complex import MAX_STIEFEL_COLS
+    ok = torch.nn.Parameter(torch.randn(2, 2, 2, 2, dtype=torch.complex128, device=dev))
+    big = torch.nn.Parameter(torch.randn(MAX_STIEFEL_COLS + 1, dtype=torch.complex128, device=dev))
+    for p in (ok, big):
+        p.grad = torch.randn_like(p)
+    before = ok.detach().clone()
+    opt = SGDG([ok, big], lr=0.1, momentum=0.9, stiefel=True)
+    random.seed(3)
+    with pytest.raises(ValueError):
+        opt.step()
+    assert random.randint(1, 101) == (random.seed(3), random.randint(1, 101))[1]
+    assert torch.equal(ok.detach(), before)
+    assert len(opt.state) == 0

@@ -86,6 +86,47 @@ def test_tree_contraction_equals_full(world):
         assert n_stages == {2: 1, 3: 2, 4: 2}[world]
 
 
+def _sub_worker(rank, world, port, q):
+    """World of 4: ranks 0-2 run a TreeContraction on their own subgroup (stage exchanges are
+    point-to-point inside it: no per-stage process groups), rank 3 never constructs one; two
+    instances on the same layout in a row."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle.contract_ref import contract
+        from tneq_qc_amd.distributed import TreeContraction
+        sub = dist.new_group([0, 1, 2])   # every world rank enters the subgroup's own creation
+        if rank < 3:
+            eq, shapes, ops = _network()
+            full = contract(eq, *ops)
+            errs = []
+            for _ in range(2):
+                job = TreeContraction(eq, shapes, group=sub, executor=_oracle_executor)
+                res = job(*[torch.from_numpy(o) for o in ops]).numpy()
+                errs.append(float(np.abs(res - full).max() / np.abs(full).max()))
+            q.put((rank, max(errs)))
+        else:
+            q.put((rank, 0.0))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tree_contraction_on_a_subgroup():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sub_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = sorted(q.get(timeout=5) for _ in range(4))
+    for rank, err in got:
+        assert err < 1e-12, (rank, err)
+
+
 def test_partition_rule_matches_reference():
     from tneq_qc_amd.distributed import partition_terms
     assert partition_terms(35, 4) == [list(range(0, 9)), list(range(9, 18)), list(range(18, 27)),
