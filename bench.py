@@ -173,26 +173,33 @@ def permute_probe(dev, rank: int = 26, reps: int = 5):
             "bit_exact": ok}
 
 
-def c5_train(dev, with_cpu: bool = True, steps: int = 20, warmup: int = 5):
+def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int = 0, rank: int = 0):
     """Secondary line (BASELINE.json configs[4], C5): the symmetry-breaking training step —
-    8 pruning candidates x (core-only forward, fidelity loss, reverse-mode backward, SGDG) in
-    complex128, each candidate on its own stream — next to the same step on the host CPU.
-    Runs scripts/c5_bench.py in a child process (started without exec): a fresh caching
-    allocator, so the candidates' buffers (and the hipGraphs keyed on their pointers) settle
-    during the warmup instead of inheriting the C4 run's pool."""
+    8 pruning candidates x (split/merge core-only forward, fidelity loss, reverse-mode backward,
+    SGDG) in complex128, each candidate on its own stream; on N ranks candidate k runs on rank
+    k mod N (every rank of this bench runs its share) — next to the same step on the host CPU.
+    Runs scripts/c5_bench.py in a child process per rank (started without exec, inheriting
+    RANK / WORLD_SIZE / LOCAL_RANK): a fresh caching allocator, so the candidates' buffers (and
+    the hipGraphs keyed on their pointers) settle during the warmup instead of inheriting the C4
+    run's pool."""
     import subprocess
-    del dev
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "c5_bench.py"), "--steps", str(steps),
-           "--warmup", str(warmup), "--cpu-steps", "1" if with_cpu else "0"]
+           "--warmup", str(warmup), "--cpu-steps", "1" if with_cpu else "0", "--port", str(port)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if rank != 0:
+        return None
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
     out = {"metric": "candidate training steps/s (forward + backward + SGDG), C5 ansatz, 8 candidates",
            "value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": steps,
-           "warmup": warmup, "dtype": d["dtype"], "cores_per_candidate": d["cores_per_candidate"],
-           "streams": d.get("streams", 1), "amplitudes_per_forward": d["amplitudes_per_forward"],
-           "bound": "latency (2^16-element tensors; ~100 dependent pairwise launches per candidate-step; "
-                    "the 8 candidates' chains overlap on 8 streams)"}
+           "warmup": warmup, "n_gpus": d.get("n_gpus", 1), "candidates_per_rank": d.get("candidates_per_rank"),
+           "dtype": d["dtype"], "cores_per_candidate": d["cores_per_candidate"],
+           "streams": d.get("streams", 1), "forward": d.get("forward"),
+           "amplitudes_per_forward": d["amplitudes_per_forward"],
+           "host_issue_ms_per_step": d.get("host_issue_ms_per_step"),
+           "wall_ms_per_step_per_rank": d.get("wall_ms_per_step_per_rank"),
+           "bound": "latency / host issue (2^16-element tensors; ~100 dependent pairwise launches per "
+                    "candidate-step; a rank's candidates overlap on their own streams)"}
     if "cpu_baseline" in d:
         out["cpu_baseline"] = dict(d["cpu_baseline"], cpu_model=_cpu_model())
     return out
@@ -471,9 +478,12 @@ def main():
                 res[key] = alt_gemm(args, var, desc)
             except Exception as e:  # the alternate lines must never hide the headline
                 res[key] = {"error": repr(e)}
-    if world == 1 and rank == 0 and not args.no_c5:
+    if not args.no_c5:   # every rank runs its share of the candidates
         try:
-            res["c5_train"] = c5_train(dev, with_cpu=not args.no_cpu_baseline)
+            port = int(os.environ.get("MASTER_PORT", "29500")) + 7
+            c5 = c5_train(with_cpu=world == 1 and not args.no_cpu_baseline, port=port, rank=rank)
+            if rank == 0:
+                res["c5_train"] = c5
         except Exception as e:  # the secondary line must never hide the headline
             res["c5_train"] = {"error": repr(e)}
     if rank == 0:

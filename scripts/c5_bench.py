@@ -7,8 +7,19 @@ train.py:30-masked ansatz (15 cores); 8 pruning candidates = the full ansatz min
 (the first round of symmetry_breaking(): candidate = [idx], 34 cores), each fitted with
 SGDG(lr=1e-2, stiefel=True, momentum=0.9).  A step = for every candidate: core-only forward
 (2^16 amplitudes), fidelity loss, backward (reverse mode through the pairwise path), one SGDG
-step.  Metric: candidate training steps/s (8 per step).  On N GPUs the candidates are split
-across ranks (weak scaling, no collective: candidates are independent fits).
+step.  Metric: candidate training steps/s (8 per step).
+
+Forward = the split/merge contractor path (BASELINE.json configs[4]; examples/
+example_qctn_merge_split.py:59-66): every candidate's QCTN is split by QCTN.split (qctn.py:
+1296-1401, cores[:n//2] | cores[n//2:]), each half is swept on its own and the halves are joined
+by the boundary contraction (einsum.partition_path), all in one native plan per candidate.
+
+Ranks: under a launcher (RANK / WORLD_SIZE / LOCAL_RANK set, as bench.py's ranks pass on) the 8
+candidates are dealt round-robin over the ranks (candidate k on rank k mod N: independent fits,
+no collective on the data path, the reference's loop symmetry_breaking_quantum.py:196-238 run
+concurrently); a gloo group on --port only times the step (barrier + max over ranks).  The line
+splits the step time into host issue time (the Python / launch work until the last candidate's
+launches are queued) and the wall time (until the GPU is done).
 
 CPU baseline ("port"): the same step with torch on the host — pairwise torch.tensordot along the
 same path (what opt_einsum's ContractExpression executes), torch autograd, and the reference's
@@ -16,6 +27,7 @@ SGDG math (oracle/optim_ref.py) — timed on a bounded sample.
     python scripts/c5_bench.py [--steps 20] [--warmup 3] [--cpu-steps 3]
 """
 import argparse
+import datetime
 import json
 import os
 import random
@@ -28,25 +40,42 @@ import torch  # noqa: E402
 
 from tneq_qc_amd.circuits import BrickWall, TRAIN_MASK  # noqa: E402
 from tneq_qc_amd.contractor import EinsumStrategy  # noqa: E402
+from tneq_qc_amd.einsum import parse_equation, partition_path  # noqa: E402
+from tneq_qc_amd.expression import HipContractExpression  # noqa: E402
 from tneq_qc_amd.optim import SGDG  # noqa: E402
 
 N_Q, DEPTH = 8, 10
 CANDIDATES = [0, 1, 4, 6, 7, 10, 11, 16]   # cores outside the target mask
 
 
-def setup(dev):
+def split_merge_expression(qctn):
+    """The core-only expression (einsum_strategy.py:136-194) contracted along QCTN.split's two
+    halves: each half swept, then the boundary contraction (the merge)."""
+    eq, sh = EinsumStrategy.build_core_only_expression(qctn)
+    left, right = qctn.split()
+    idx = {c: i for i, c in enumerate(qctn.cores)}
+    groups = [[idx[c] for c in left.cores], [idx[c] for c in right.cores]]
+    return HipContractExpression(eq, *sh, optimize=partition_path(parse_equation(eq, sh), groups)), eq
+
+
+def setup(dev, ks=None):
     tgt_bw = BrickWall(N_Q, DEPTH, seed=5, mask=TRAIN_MASK)
     eq_t, sh_t = EinsumStrategy.build_core_only_expression(tgt_bw.qctn)
     ex_t = EinsumStrategy.create_contract_expression(eq_t, sh_t)
     target = ex_t(*[torch.from_numpy(tgt_bw.cores[c]).to(dev) for c in tgt_bw.qctn.cores]).reshape(-1)
     cands = []
     for k, idx in enumerate(CANDIDATES):
+        if ks is not None and k not in ks:
+            continue
         bw = BrickWall(N_Q, DEPTH, seed=100 + k, mask=[idx])
-        eq, sh = EinsumStrategy.build_core_only_expression(bw.qctn)
-        expr = EinsumStrategy.create_contract_expression(eq, sh)
+        expr, eq = split_merge_expression(bw.qctn)
         params = [torch.nn.Parameter(torch.from_numpy(bw.cores[c].copy()).to(dev)) for c in bw.qctn.cores]
         opt = SGDG(params, lr=1e-2, stiefel=True, momentum=0.9)
-        cands.append((expr, params, opt, bw, eq))
+        # the candidate's own stream of the SGDG retraction draws (the global `random` the
+        # reference draws from is swapped in around its step): results independent of the rank
+        # layout
+        rstate = [random.Random(1000 + k).getstate()]
+        cands.append((expr, params, opt, bw, eq, rstate))
     return target, cands
 
 
@@ -63,7 +92,7 @@ def gpu_step(target, cands, streams=None):
     own hipGraphs) overlap on the GPU instead of queueing behind each other."""
     losses = []
     cur = torch.cuda.current_stream()
-    for k, (expr, params, opt, _, _) in enumerate(cands):
+    for k, (expr, params, opt, _, _, rstate) in enumerate(cands):
         st = streams[k] if streams else cur
         if streams:
             st.wait_stream(cur)
@@ -71,7 +100,9 @@ def gpu_step(target, cands, streams=None):
             opt.zero_grad()
             loss = fidelity_loss(expr(*params), target)
             loss.backward()
+            random.setstate(rstate[0])
             opt.step()
+            rstate[0] = random.getstate()
         losses.append(loss)
     if streams:
         for st in streams:
@@ -85,7 +116,7 @@ def cpu_step_sample(target_np, cands, steps):
     from tneq_qc_amd.einsum import _State
     tgt = torch.from_numpy(target_np)
     items = []
-    for expr, params, _, bw, _ in cands:
+    for expr, params, _, bw, _, _ in cands:
         items.append((expr, [p.detach().cpu().numpy().copy() for p in params], {}))
     t0 = time.perf_counter()
     n = 0
@@ -122,26 +153,64 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--one-stream", action="store_true", help="candidates one after another on one stream")
+    ap.add_argument("--port", type=int, default=0, help="gloo timing group port (multi-rank)")
     a = ap.parse_args()
-    dev = torch.device("cuda:0")
-    random.seed(0)
-    target, cands = setup(dev)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method=f"tcp://{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{a.port}",
+                                rank=rank, world_size=world, timeout=datetime.timedelta(seconds=240))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    random.seed(rank)
+    mine = list(range(rank, len(CANDIDATES), world))
+    target, cands = setup(dev, set(mine))
     streams = None if a.one_stream else [torch.cuda.Stream(dev) for _ in cands]
     for _ in range(a.warmup):
         gpu_step(target, cands, streams)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         losses = gpu_step(target, cands, streams)
+    t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / a.steps
+    dt_local = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    times = torch.tensor([dt, dt_local, t_issue], dtype=torch.float64)
+    my_losses = {int(k): float(l.detach()) for k, l in zip(mine, losses)}
+    if world > 1:
+        allt = [torch.zeros_like(times) for _ in range(world)]
+        dist.all_gather(allt, times)
+        dt = max(float(t[0]) for t in allt)
+        parts = [None] * world
+        dist.all_gather_object(parts, my_losses)
+        for d in parts:
+            my_losses.update(d)
+    else:
+        allt = [times]
+    dt /= a.steps
     res = {"metric": "candidate training steps/s (forward + backward + SGDG), C5 ansatz",
-           "value": len(cands) / dt, "unit": "candidate-steps/s", "ms_per_step": dt * 1e3,
-           "candidates": len(cands), "cores_per_candidate": len(cands[0][1]), "dtype": "c128",
+           "value": len(CANDIDATES) / dt, "unit": "candidate-steps/s", "ms_per_step": dt * 1e3,
+           "n_gpus": world, "candidates": len(CANDIDATES),
+           "candidates_per_rank": [len(range(r, len(CANDIDATES), world)) for r in range(world)],
+           "cores_per_candidate": len(cands[0][1]), "dtype": "c128",
            "streams": len(streams) if streams else 1,
+           "forward": "QCTN.split halves swept + boundary contraction (split/merge path), one native plan",
            "amplitudes_per_forward": int(np.prod(cands[0][0].out_shape)),
-           "loss_after": [float(l.detach()) for l in losses]}
-    if a.cpu_steps > 0:
+           "host_issue_ms_per_step": [float(t[2]) / a.steps * 1e3 for t in allt],
+           "wall_ms_per_step_per_rank": [float(t[1]) / a.steps * 1e3 for t in allt],
+           "loss_after": [my_losses[k] for k in sorted(my_losses)]}
+    if world > 1:
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    if a.cpu_steps > 0 and world == 1:
         # every host core and 16 (the box's CPU share per GPU): the faster counts
         host = os.cpu_count() or 1
         runs = []
