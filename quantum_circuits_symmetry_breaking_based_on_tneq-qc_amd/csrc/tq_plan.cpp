@@ -1016,6 +1016,7 @@ class Compiler {
       digits(t, sh.tin, dig);
       int64_t o = 0;
       for (int m : sh.tin) o += dig[m] * sx[m];
+      if (o >= (int64_t(1) << 31)) return false;   // staged as int32 by the kernel
       dd->in_off[t] = o;
     }
     for (int64_t t = 0; t < sh.tout_n; ++t) {

@@ -158,9 +158,9 @@ struct S2DLaunch {
   int nops = 0, pad = 0;
   S2DOp op[kS2MaxOps];
 };
-// blocks of a dense op (4 waves each, one 64-column group per wave and iteration)
+// blocks of a dense op (4 waves each, one 32-column tile per wave and iteration)
 inline int s2d_blocks(int64_t ncols) {
-  const int64_t tiles = ncols / 64;
+  const int64_t tiles = ncols / 32;
   const int64_t b = (tiles + 3) / 4;
   return (int)(b < 256 ? b : 256);
 }

@@ -14,11 +14,19 @@
 //     HBM: a half-wave reads 32 consecutive columns = 256 B; the plan only picks ops whose six
 //     lowest column bits are the memory-fastest bits of X and Y);
 //   * Gauss's 3M product (P1 = Mr Xr, P2 = Mi Xi, P3 = (Mr + Mi)(Xr + Xi); Dr = P1 - P2,
-//     Di = P3 - P1 - P2): 3 MFMAs per k-step and 32 x 32 tile; the sums Mr + Mi are an LDS plane
-//     of their own, Xr + Xi are formed once per column tile;
-//   * a wave owns a 64-column group at a time, loads its tin inputs once and streams every
-//     32-output tile of both 32-column halves out of the accumulators (lane -> column: a store
-//     instruction writes two 256-B row segments; a row's two halves leave back to back).
+//     Di = P3 - P1 - P2): 3 MFMAs per k-step and 32 x 32 tile; the sums Mr + Mi and Xr + Xi
+//     are formed in registers;
+//   * a wave owns a 32-column tile at a time (inputs loaded once, column bases from small LDS
+//     tables) and streams every 32-output tile out of the accumulators; lane pairs trade one
+//     value per two rows so that every lane stores 16 B (two columns of one row): 4 x 256-B row
+//     segments per store instruction.
+// Measured (C4, one 4-lane launch = 2 GiB of stores): 450-490 us, ~4.5 TB/s, against 1.6 ms for the
+// same ops as sweep2 passes.  What does not bound it: the MFMAs (removed: -10 %), the stores'
+// instruction count (8-B -> 16-B stores: +-0), the tile shape (64-column groups, two output tiles
+// in flight per wave: +-0 / -15 %), a dedicated loader wave feeding the inputs through LDS
+// (-30 %: the per-round barrier aligns the waves' MFMA phases).  The tin = 8 op sits at the same
+// 450 us as tin = 16 with half the MFMA work: the output stream itself (2^21 separate 256-B row
+// segments per op, each written once) runs at ~4.5 TB/s, where a linear fill reaches 6.35 TB/s.
 // A first version on the vector ALUs (coefficients by scalar loads) ran 1.9-4.7 TB/s: the
 // tout x tin coefficients (32 KiB at tin 16) stream through the scalar cache once per column
 // group.  Algorithmic bytes per op = (numel(X) + numel(Y)) * 8; 8 * tin flops per output.
@@ -53,90 +61,126 @@ __device__ __forceinline__ f2v f16_terms(f2v v, int sc) {
   return f2v{__uint_as_float(h), __uint_as_float(__builtin_bit_cast(uint32_t, lv))};
 }
 
-constexpr int kWaves = 4;   // waves per workgroup
+constexpr int kWaves = 4;             // waves per workgroup
+constexpr int kLevels = 7;            // column-base tables: 6 column bits each, bits 6 .. 47
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 template <int TIN>
 __global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
   static_assert(TIN % 2 == 0 && TIN <= kS2DMaxTin, "k-steps of 2");
   constexpr int KS = TIN / 2;
-  __shared__ float mp[3][TIN * kS2DMaxTout];   // planes Mr, Mi, Mr + Mi as [k][r]
-  __shared__ int32_t ooff[kS2DMaxTout];        // output offsets (elements)
+  __shared__ float mp[2][TIN * kS2DMaxTout];     // planes Mr, Mi as [k][r]
+  __shared__ int32_t ooff[kS2DMaxTout];          // output offsets (elements)
+  __shared__ int64_t btab[2][kLevels][64];       // column-group bases (in, out) per 6-bit level
+  __shared__ int64_t wcol[2][kS2MaxColBits];
   int j = 0;
   for (int q = 1; q < L.nops; ++q)
     if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
   const S2DOp& op = L.op[j];
   cst<S2Dense>* d = as_const<S2Dense>(op.desc);
   const int tout = d->tout, colbits = d->colbits;
+  const int tid = threadIdx.x;
   {
     const float2* M = reinterpret_cast<const float2*>(op.M);   // [r][k], written by the compose op
-    for (int i = threadIdx.x; i < tout * TIN; i += 64 * kWaves) {
-      const int r = i / TIN, k = i % TIN;
-      const float2 v = M[i];
+    for (int i = tid; i < tout * TIN; i += 64 * kWaves) {
+      const int r = i % tout, k = i / tout;                    // LDS-write order: conflict-free
+      const float2 v = M[r * TIN + k];
       mp[0][k * tout + r] = v.x;
       mp[1][k * tout + r] = v.y;
-      mp[2][k * tout + r] = v.x + v.y;
     }
-    for (int r = threadIdx.x; r < tout; r += 64 * kWaves) ooff[r] = (int32_t)d->out_off[r];
+    for (int r = tid; r < tout; r += 64 * kWaves) ooff[r] = (int32_t)d->out_off[r];
+    for (int i = tid; i < 2 * kS2MaxColBits; i += 64 * kWaves)
+      wcol[i / kS2MaxColBits][i % kS2MaxColBits] = (i / kS2MaxColBits) ? d->w_out[i % kS2MaxColBits] : d->w_in[i % kS2MaxColBits];
   }
   __syncthreads();
+  // btab[io][l][v] = sum of the weights of the set bits of v among column bits 6+6l .. 6+6l+5
+  for (int i = tid; i < 2 * kLevels * 64; i += 64 * kWaves) {
+    const int io = i / (kLevels * 64), l = (i / 64) % kLevels, v = i % 64;
+    int64_t acc = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int cb = 6 + 6 * l + b;
+      if (((v >> b) & 1) && cb < colbits) acc += wcol[io][cb];
+    }
+    btab[io][l][v] = acc;
+  }
+  __syncthreads();
+  auto base = [&](int io, int64_t g) {
+    int64_t b = 0;
+#pragma unroll
+    for (int l = 0; l < kLevels; ++l) b += btab[io][l][(g >> (6 * l)) & 63];
+    return b;
+  };
   const f2v* __restrict__ X = reinterpret_cast<const f2v*>(op.X);
   f2v* __restrict__ Y = reinterpret_cast<f2v*>(op.Y);
-  const int lane = threadIdx.x & 63, fr = lane & 31, fk = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ngroups = d->ncols >> 6;
+  const int lane = tid & 63, fr = lane & 31, fk = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t ntiles = d->ncols >> 5;
   const int64_t nw = (int64_t)op.nblocks * kWaves;
   const bool use_beta = op.use_beta;
   const float beta = (float)op.beta;
   const bool split = op.split_sc != nullptr;
   const int sc = split ? *op.split_sc : 0;
   const bool track = op.amax != nullptr;
+  const bool odd = lane & 1;
   float vmax = 0.f;
-  int64_t io[KS];   // this lane's input offsets: element 2s + fk of the tile
+  int32_t io[KS];   // this lane's input offsets: element 2s + fk of the tile (< 2^31, plan)
 #pragma unroll
-  for (int s = 0; s < KS; ++s) io[s] = d->in_off[2 * s + fk];
-  // a wave owns a 64-column group (two 32-column MFMA tiles, h = 0 / 1): every 32-output tile
-  // is computed and stored for both halves back to back, so the two 256-B halves of each
-  // 512-B output row segment leave within a few hundred cycles of each other
-  for (int64_t g = (int64_t)((int)blockIdx.x - op.block_begin) * kWaves + wave; g < ngroups; g += nw) {
-    int64_t bi = 0, bo = 0;
-    for (int b = 6; b < colbits; ++b)
-      if ((g >> (b - 6)) & 1) { bi += d->w_in[b]; bo += d->w_out[b]; }
-    float xr[2][KS], xi[2][KS], xs[2][KS];
+  for (int s = 0; s < KS; ++s) io[s] = (int32_t)d->in_off[2 * s + fk];
+  // one 32-output tile's results (Cr, Ci accumulators) out as 16-B stores: accumulator e of a
+  // lane is output row rt + (e & 3) + 8 (e >> 2) + 4 fk, column fr; rows of e and e + 1 are
+  // adjacent, so the lane pair (2i, 2i+1) trades one value and the even lane stores row(e), the
+  // odd lane row(e+1), both columns
+  auto emit = [&](const f32x16& cr, const f32x16& ci, const f2v* Yt, int rt) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int e = 0; e < 16; e += 2) {
+      const f2v v0 = {cr[e], ci[e]};
+      const f2v v1 = {cr[e + 1], ci[e + 1]};
+      if (track) vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v1.x), fabsf(v1.y))));
+      const f2v send = odd ? v0 : v1;
+      f2v recv;   // quad_perm [1, 0, 3, 2]: the partner lane's value
+      recv.x = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send.x), 0xB1, 0xF, 0xF, false));
+      recv.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send.y), 0xB1, 0xF, 0xF, false));
+      f4v w = odd ? f4v{recv.x, recv.y, v1.x, v1.y} : f4v{v0.x, v0.y, recv.x, recv.y};
+      const int r = rt + (e & 3) + 8 * (e >> 2) + 4 * fk + (odd ? 1 : 0);
+      f4v* p = reinterpret_cast<f4v*>(const_cast<f2v*>(Yt) + ooff[r]);
+      if (use_beta) w += *p * beta;
+      if (split) {
+        const f2v a = f16_terms(f2v{w.x, w.y}, sc), b = f16_terms(f2v{w.z, w.w}, sc);
+        w = f4v{a.x, a.y, b.x, b.y};
+      }
+      if (op.pad != 2) *p = w;   // development diagnostic (TQ_S2D_DIAG=2): no stores
+      else if (w.x == 12345.f) *p = w;
+    }
+  };
+  for (int64_t t = (int64_t)((int)blockIdx.x - op.block_begin) * kWaves + wave; t < ntiles; t += nw) {
+    // column tile t: columns 32t .. 32t+31 (bits 0..4 = lane, bit 5 = t & 1, bits >= 6: tables)
+    const int64_t g = t >> 1;
+    const int cl = (int)(t & 1) * 32 + fr;
+    const int64_t bi = base(0, g);
+    float xr[KS], xi[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f2v v = X[bi + io[s] + cl];
+      xr[s] = v.x;
+      xi[s] = v.y;
+    }
+    const f2v* Yt = Y + (base(1, g) + (cl & ~1));   // a lane pair stores columns (cl & ~1), +1
+    // one 32-output tile per iteration; Gauss's 3M product (three accumulator sets)
+    for (int rt = 0; rt < tout; rt += 32) {
+      f32x16 p1 = {}, p2 = {}, p3 = {};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const f2v v = X[bi + io[s] + h * 32 + fr];
-        xr[h][s] = v.x;
-        xi[h][s] = v.y;
-        xs[h][s] = v.x + v.y;
+        if (op.pad == 1) break;   // development diagnostic (TQ_S2D_DIAG=1): no MFMAs
+        const int a = (2 * s + fk) * tout + rt + fr;
+        const float mr = mp[0][a], mi = mp[1][a];
+        p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(mr, xr[s], p1, 0, 0, 0);
+        p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(mi, xi[s], p2, 0, 0, 0);
+        p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(mr + mi, xr[s] + xi[s], p3, 0, 0, 0);
       }
-    for (int rt = 0; rt < tout; rt += 32) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f32x16 p1 = {}, p2 = {}, p3 = {};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const int a = (2 * s + fk) * tout + rt + fr;
-          p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[0][a], xr[h][s], p1, 0, 0, 0);
-          p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[1][a], xi[h][s], p2, 0, 0, 0);
-          p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(mp[2][a], xs[h][s], p3, 0, 0, 0);
-        }
-        // accumulator e of a lane: output row rt + (e & 3) + 8 (e >> 2) + 4 fk, column h*32 + fr
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int r = rt + (e & 3) + 8 * (e >> 2) + 4 * fk;
-          f2v v = {p1[e] - p2[e], p3[e] - p1[e] - p2[e]};
-          f2v* p = Y + (bo + ooff[r] + h * 32 + fr);
-          if (use_beta) v += *p * beta;
-          if (track) vmax = fmaxf(vmax, fmaxf(fabsf(v.x), fabsf(v.y)));
-          *p = split ? f16_terms(v, sc) : v;
-          // keeps the 16 store addresses from being formed (and held) all at once
-          if ((e & 3) == 3) asm volatile("" ::: "memory");
-        }
-      }
+      emit(p1 - p2, p3 - p1 - p2, Yt, rt);
     }
   }
   if (track) {
@@ -157,7 +201,6 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     set_error("sweepd: bad op count");
     return TQ_ERR_INVALID;
   }
-  int blocks = 0;
   const int tin = L.op[0].tin;
   for (int q = 0; q < L.nops; ++q) {
     if (L.op[q].tin != tin) {
@@ -169,17 +212,45 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
       set_error("sweepd: bad output tile");
       return TQ_ERR_INVALID;
     }
-    blocks = std::max(blocks, L.op[q].block_begin + L.op[q].nblocks);
   }
-  if (blocks <= 0) return TQ_OK;
+  // one round of resident workgroups over the launch's ops (the kernel strides over its tiles):
+  // a second, partial round of workgroups left most CUs idle (1024 blocks on 768 slots)
+  const void* fn = nullptr;
   switch (tin) {
-    case 2: hipLaunchKernelGGL(sweepd_kernel<2>, dim3(blocks), dim3(64 * kWaves), 0, stream, L); break;
-    case 4: hipLaunchKernelGGL(sweepd_kernel<4>, dim3(blocks), dim3(64 * kWaves), 0, stream, L); break;
-    case 8: hipLaunchKernelGGL(sweepd_kernel<8>, dim3(blocks), dim3(64 * kWaves), 0, stream, L); break;
-    case 16: hipLaunchKernelGGL(sweepd_kernel<16>, dim3(blocks), dim3(64 * kWaves), 0, stream, L); break;
+    case 2: fn = reinterpret_cast<const void*>(&sweepd_kernel<2>); break;
+    case 4: fn = reinterpret_cast<const void*>(&sweepd_kernel<4>); break;
+    case 8: fn = reinterpret_cast<const void*>(&sweepd_kernel<8>); break;
+    case 16: fn = reinterpret_cast<const void*>(&sweepd_kernel<16>); break;
     default:
       set_error("sweepd: tin must be 2, 4, 8 or 16");
       return TQ_ERR_INVALID;
+  }
+  static int slots[kS2DMaxTin + 1] = {};
+  if (!slots[tin]) {
+    int dev = 0, cus = 0, per = 0;
+    TQ_HIP(hipGetDevice(&dev));
+    TQ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    TQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kWaves, 0));
+    slots[tin] = std::max(1, cus * std::max(1, per));
+  }
+  S2DLaunch R = L;
+  static const int diag = [] {
+    const char* e = getenv("TQ_S2D_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  int blocks = 0;
+  for (int q = 0; q < R.nops; ++q) {
+    const int want = std::max(1, slots[tin] / R.nops);
+    R.op[q].nblocks = std::max(1, std::min(R.op[q].nblocks, want));
+    R.op[q].block_begin = blocks;
+    R.op[q].pad = diag;
+    blocks += R.op[q].nblocks;
+  }
+  switch (tin) {
+    case 2: hipLaunchKernelGGL(sweepd_kernel<2>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
+    case 4: hipLaunchKernelGGL(sweepd_kernel<4>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
+    case 8: hipLaunchKernelGGL(sweepd_kernel<8>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
+    default: hipLaunchKernelGGL(sweepd_kernel<16>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
   }
   TQ_HIP(hipGetLastError());
   return TQ_OK;
