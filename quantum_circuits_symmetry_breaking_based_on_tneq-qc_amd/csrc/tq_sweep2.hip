@@ -719,6 +719,33 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
   int blocks = 0;
   for (int q = 0; q < L.nops; ++q) blocks = std::max(blocks, L.op[q].block_begin + L.op[q].nblocks);
   if (blocks <= 0) return TQ_OK;
+  // Opt-in (TQ_S2_CAP=1): a launch of more workgroups than fit on the GPU at once (the
+  // lane-merged per-slice levels: 8 ops x 512 chunks) scaled to one resident round, every
+  // workgroup striding over more chunks -- to amortize the ~5-us workgroup prologue.  Measured on
+  // C4: 295 vs 276 us for the 4096-workgroup level (the extra rounds overlap their prologues with
+  // the previous round's chunks), so it stays off.
+  static const int cap = [] {
+    const char* e = getenv("TQ_S2_CAP");
+    if (!e || e[0] != '1') return 0;
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&sweep2_kernel<T, CB>), NT, 0) != hipSuccess)
+      return 0;
+    return cus * std::max(1, per);
+  }();
+  if (cap > 0 && blocks > cap) {
+    S2Launch R = L;
+    int b = 0;
+    for (int q = 0; q < R.nops; ++q) {
+      R.op[q].nblocks = std::max(1, (int)((int64_t)L.op[q].nblocks * cap / blocks));
+      R.op[q].block_begin = b;
+      b += R.op[q].nblocks;
+    }
+    hipLaunchKernelGGL((sweep2_kernel<T, CB>), dim3((unsigned)b), dim3(NT), 0, stream, R);
+    TQ_HIP(hipGetLastError());
+    return TQ_OK;
+  }
   hipLaunchKernelGGL((sweep2_kernel<T, CB>), dim3((unsigned)blocks), dim3(NT), 0, stream, L);
   TQ_HIP(hipGetLastError());
   return TQ_OK;
