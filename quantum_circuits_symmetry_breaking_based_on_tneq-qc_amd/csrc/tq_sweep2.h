@@ -159,10 +159,13 @@ struct S2DLaunch {
   S2DOp op[kS2MaxOps];
 };
 // blocks of a dense op (4 waves each, one 32-column tile per wave and iteration)
+// workgroups a dense op may use (4 waves, one 32-column tile per wave at a time); the launcher
+// caps the launch at one round of resident workgroups shared by its ops (a single-lane op then
+// gets all of them: 1 workgroup per CU left 3 of 4 slots idle at 3.0 TB/s)
 inline int s2d_blocks(int64_t ncols) {
   const int64_t tiles = ncols / 32;
   const int64_t b = (tiles + 3) / 4;
-  return (int)(b < 256 ? b : 256);
+  return (int)(b < 2048 ? b : 2048);
 }
 int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream);
 int sweep2_timing(unsigned long long* out, int n);   // development instrumentation

@@ -121,6 +121,31 @@ __device__ __forceinline__ f2v pmac(f2v acc, f2v a, f2v b) {
   return acc;
 }
 
+// a * b on packed f32 (the first product of a sum: no zeroed accumulator to initialise)
+__device__ __forceinline__ f2v pmul(f2v a, f2v b) {
+  f2v acc;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(acc) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "+v"(acc) : "v"(a), "v"(b));
+  return acc;
+}
+
+template <typename T>
+__device__ __forceinline__ T mul(const T& a, const T& b) {
+#if defined(TQ_S2_DIAG) && TQ_S2_DIAG == 1
+  (void)b;
+  return a;
+#endif
+  if constexpr (std::is_same<T, c64>::value) {
+    const f2v r = pmul(f2v{a.re, a.im}, f2v{b.re, b.im});
+    return c64{r.x, r.y};
+  } else {
+    T acc = tzero<T>();
+    cmac(acc, a, b);
+    return acc;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void mac(T& acc, const T& a, const T& b) {
 #if defined(TQ_S2_DIAG) && TQ_S2_DIAG == 1
@@ -196,9 +221,9 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        T acc = tzero<T>();
+        T acc = mul(x[u][0], c[0]);
 #pragma unroll
-        for (int k = 0; k < K; ++k) mac(acc, x[u][k], c[k]);
+        for (int k = 1; k < K; ++k) mac(acc, x[u][k], c[k]);
         if (ok[u]) *reinterpret_cast<T*>(bb + (a0[u] ^ na[n])) = acc;
       }
     }
@@ -231,11 +256,21 @@ __device__ __forceinline__ T uniform(T v) {
   return u.t;
 }
 
+// Coefficients are wave-uniform.  complex64: read from LDS at a uniform address straight into
+// VGPRs (broadcast) -- the packed FMAs take VGPR operands only, so scalar copies (readfirstlane)
+// would be moved back into VGPRs before every use, 2 extra VALU instructions per dword.  Other
+// types: scalar registers (the FMAs read them directly; VGPRs are what the 16-element blocks
+// need).
+template <typename T>
+__device__ __forceinline__ T coef(const T* cf, int i) {
+  if constexpr (std::is_same<T, c64>::value) return cf[i];
+  else return uniform(cf[i]);
+}
 template <typename T, int B, int I, int J>
 __device__ __forceinline__ void blk_apply4(T (&x)[1 << B], const T* __restrict__ cf) {
   T c[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) c[i] = uniform(cf[i]);
+  for (int i = 0; i < 16; ++i) c[i] = coef(cf, i);
 #pragma unroll
   for (int r = 0; r < (1 << (B - 2)); ++r) {
     const int base = deposit2<B, I, J>(r);
@@ -244,9 +279,9 @@ __device__ __forceinline__ void blk_apply4(T (&x)[1 << B], const T* __restrict__
     for (int k = 0; k < 4; ++k) in[k] = x[base | ((k & 1) << I) | ((k >> 1) << J)];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      T acc = tzero<T>();
+      T acc = mul(in[0], c[n]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) mac(acc, in[k], c[k * 4 + n]);
+      for (int k = 1; k < 4; ++k) mac(acc, in[k], c[k * 4 + n]);
       x[base | ((n & 1) << I) | ((n >> 1) << J)] = acc;
     }
   }
@@ -256,15 +291,13 @@ template <typename T, int B, int I>
 __device__ __forceinline__ void blk_apply2(T (&x)[1 << B], const T* __restrict__ cf) {
   T c[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) c[i] = uniform(cf[i]);
+  for (int i = 0; i < 4; ++i) c[i] = coef(cf, i);
 #pragma unroll
   for (int r = 0; r < (1 << (B - 1)); ++r) {
     const int base = deposit2<B, I, I>(r) ;
     const T a = x[base], b = x[base | (1 << I)];
-    T y0 = tzero<T>(), y1 = tzero<T>();
-    mac(y0, a, c[0]);
+    T y0 = mul(a, c[0]), y1 = mul(a, c[1]);
     mac(y0, b, c[2]);
-    mac(y1, a, c[1]);
     mac(y1, b, c[3]);
     x[base] = y0;
     x[base | (1 << I)] = y1;
@@ -665,9 +698,9 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
         if (st_lane) {
 #pragma unroll
           for (int n = 0; n < N; ++n) {
-            T acc = tzero<T>();
+            T acc = mul(x[0], c[n]);
 #pragma unroll
-            for (int k = 0; k < K; ++k) mac(acc, x[k], c[k * N + n]);
+            for (int k = 1; k < K; ++k) mac(acc, x[k], c[k * N + n]);
             T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + n]), sto);
             const T v = use_beta ? scale_add(acc, *p, beta) : acc;
             TQ_ST(p, stored(v));

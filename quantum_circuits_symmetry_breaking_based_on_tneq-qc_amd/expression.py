@@ -13,7 +13,9 @@ contracted symbols from the inputs and sums the sub-contractions.
 from __future__ import annotations
 
 import ctypes
+import operator
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
@@ -59,10 +61,15 @@ class NativePlan:
         L.tq_plan_describe(self._h, buf, n + 1)
         return buf.value.decode()
 
-    def execute(self, ptrs: Sequence[int], out_ptr: int, stream: int, begin: int = 0,
+    @staticmethod
+    def pointer_array(ptrs: Sequence[int]):
+        return (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
+
+    def execute(self, ptrs, out_ptr: int, stream: int, begin: int = 0,
                 end: Optional[int] = None, step: int = 1, accumulate: bool = False) -> None:
+        """`ptrs`: the input base pointers (a sequence of ints, or an array from pointer_array)."""
         end = self.n_slices if end is None else end
-        arr = (ctypes.c_void_p * max(1, len(ptrs)))(*[ctypes.c_void_p(p) for p in ptrs])
+        arr = ptrs if isinstance(ptrs, ctypes.Array) else self.pointer_array(ptrs)
         rc = _lib.lib().tq_plan_execute(self._h, arr, ctypes.c_void_p(out_ptr), begin, end, step,
                                         int(accumulate), ctypes.c_void_p(stream))
         check(rc, "tq_plan_execute")
@@ -132,6 +139,7 @@ class HipContractExpression:
             self.n_slices *= self.net.extents[m]
         self._plans: Dict[tuple, NativePlan] = {}
         self._lock = threading.Lock()
+        self._bound = None   # operands of the last call (see _forward's fast path)
 
     # -- introspection ---------------------------------------------------------------------
     @property
@@ -201,8 +209,31 @@ class HipContractExpression:
         self._plans[key] = (g, bcast)
         return g, bcast
 
+    def _bound_call(self, tensors):
+        """(plan, pointer array, device, dtype) when `tensors` are the very objects of the last
+        validated call, unmodified since: same data pointers, strides, shapes and version
+        counters (every in-place op, the metadata ones included, bumps them; a lazy conj / neg
+        bit cannot appear on an existing tensor object except through ``.data`` reassignment,
+        which -- as for autograd's version checks -- is not tracked).  A network of hundreds of
+        cores (C4: 606 operands) is then re-bound in ~0.3 ms instead of the ~2 ms per-operand
+        conversion + validation pass."""
+        b = self._bound
+        if b is None or len(tensors) != len(b[0]):
+            return None
+        objs, vers, ptrs, strides, shapes, hit = b
+        if not all(r() is t for r, t in zip(objs, tensors)):
+            return None
+        if ([t._version for t in tensors] != vers or [t.data_ptr() for t in tensors] != ptrs
+                or [t.stride() for t in tensors] != strides or [t.shape for t in tensors] != shapes):
+            return None
+        return hit
+
     def _forward(self, *tensors, out: Optional[torch.Tensor] = None, slice_range=None,
                  accumulate: bool = False) -> torch.Tensor:
+        hit = self._bound_call(tensors)
+        if hit is not None:
+            plan, arr, dev, dt = hit
+            return self._run(plan, arr, dev, dt, out, slice_range, accumulate)
         if len(tensors) != len(self.net.terms):
             raise ValueError(f"expression takes {len(self.net.terms)} operands, got {len(tensors)}")
         ts = [t if isinstance(t, torch.Tensor) else torch.as_tensor(t) for t in tensors]
@@ -223,6 +254,18 @@ class HipContractExpression:
         strides = [t.stride() for t in ts]
         contiguous = all(t.is_contiguous() for t in ts)
         plan = self.plan(dt, None if contiguous else strides, dev.index)
+        ptrs = [t.data_ptr() for t in ts]
+        arr = plan.pointer_array(ptrs)
+        # remembered only when the plan reads the caller's own tensors (no converted copies)
+        if all(map(operator.is_, ts, tensors)):
+            # weak references: the binding does not keep the caller's operands alive
+            self._bound = (tuple(map(weakref.ref, ts)), [t._version for t in ts], ptrs, strides,
+                           [t.shape for t in ts], (plan, arr, dev, dt))
+        else:
+            self._bound = None
+        return self._run(plan, arr, dev, dt, out, slice_range, accumulate)
+
+    def _run(self, plan: NativePlan, arr, dev, dt, out, slice_range, accumulate) -> torch.Tensor:
         if out is None:
             out = torch.empty(self.out_shape, dtype=dt, device=dev)
             accumulate = False
@@ -232,7 +275,7 @@ class HipContractExpression:
         begin, end, step = (0, plan.n_slices, 1) if slice_range is None else slice_range
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
-            plan.execute([t.data_ptr() for t in ts], out.data_ptr(), stream, begin, end, step, accumulate)
+            plan.execute(arr, out.data_ptr(), stream, begin, end, step, accumulate)
         return out
 
 

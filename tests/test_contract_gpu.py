@@ -260,3 +260,39 @@ def test_engine_contract_with_vector_inputs(dev, dtype):
     eq_q, _ = qctn_ref.build_with_qctn_expression(qr, qr)
     cores = [bw.cores[c] for c in qr.cores]
     assert _err(ov, ref_contract(eq_q, *cores, *cores)) < TOL[dtype]
+
+
+def test_operand_binding_fast_path_tracks_changes(dev):
+    """Repeated calls with the same operand objects take the bound fast path; an in-place update,
+    an in-place transpose (strides), a replaced operand or a converted copy must all be seen."""
+    import torch
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task
+    from tneq_qc_amd.expression import HipContractExpression
+    t = amplitude_task(BrickWall(10, 6, 11), list(range(3, 7)))
+    e = HipContractExpression(t.eq, *t.shapes, optimize=t.path)
+    ts = [torch.from_numpy(np.ascontiguousarray(o)).to(dev, torch.complex128) for o in t.operands]
+    ops = [np.array(o, dtype=np.complex128) for o in t.operands]
+
+    def check():
+        out = e(*ts).cpu().numpy()
+        assert _err(out, ref_contract(t.eq, *ops)) < 1e-12
+
+    check()
+    assert e._bound is not None and e._bound_call(tuple(ts)) is not None
+    check()                                          # fast path, same result
+    sq = next(i for i, o in enumerate(ops) if o.ndim == 4)
+    ts[sq].mul_(0.5 + 0.25j)                          # in place: version bump
+    ops[sq] = ops[sq] * (0.5 + 0.25j)
+    check()
+    ts[sq].transpose_(0, 1)                           # metadata: strides change
+    ops[sq] = ops[sq].transpose(1, 0, 2, 3)
+    check()
+    k = next(i for i, o in enumerate(ops) if o.ndim == 4 and i != sq)
+    ts[k] = ts[k] * 2                                 # a different object
+    ops[k] = ops[k] * 2
+    check()
+    # operands the call converts (complex64 -> complex128) are not bound
+    ts64 = [x.to(torch.complex64) for x in ts]
+    e2 = HipContractExpression(t.eq, *t.shapes, optimize=t.path)
+    e2(*[x.to(torch.complex128) if i else ts64[0] for i, x in enumerate(ts)])
+    assert e2._bound is None
