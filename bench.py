@@ -46,6 +46,14 @@ PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 N_OPEN_CPU = 20                 # open outputs in the CPU-baseline sample (one slice: ~5-15 s of numpy)
 
 
+_T0 = time.perf_counter()
+
+
+def _log(msg: str) -> None:
+    """Progress on stderr (the JSON line stays the only stdout line): one line per phase."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def _profile_json(name: str, config: str):
     """A committed rocprofv3 PMC summary under profiles/ (or None)."""
     path = os.path.join(ROOT, "profiles", name)
@@ -120,6 +128,7 @@ def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
     n_amp = t.n_amplitudes
     runs = []
     for th in sorted({host, min(16, host)}, reverse=True):
+        _log(f"cpu baseline at {th} BLAS threads")
         done, dt, used = _cpu_sample(t, n_sl, min_seconds if th == host else min_seconds / 2, th)
         runs.append({"value": n_amp / (n_sl * dt / done), "cores": used,
                      "sample": f"{done} of {n_sl} slices timed ({dt:.2f} s)"})
@@ -185,7 +194,8 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "c5_bench.py"), "--steps", str(steps),
            "--warmup", str(warmup), "--cpu-steps", "1" if with_cpu else "0", "--port", str(port)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    # stdout carries the child's JSON line; its stderr (progress) passes through
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=300)
     if rank != 0:
         return None
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
@@ -309,6 +319,7 @@ def main():
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    _log(f"plan compiled in {t_plan:.1f} s ({n_slices} slices); warmup")
     for _ in range(args.warmup):
         step()
     # ---- headline: production path (hipGraph replay per step, no events)
@@ -322,6 +333,7 @@ def main():
         import numpy as np
         np.save(args.save_out, out.cpu().numpy())
 
+    _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step")
     # ---- dominant kernel: the same K steps launched eagerly with HIP events around every GEMM
     plan.profile(_lib.TQ_OP_GEMM)
     dt_prof = timed(args.steps)
@@ -340,7 +352,7 @@ def main():
     g3m = bool(L.tq_library_query(b"gemm_3m") == 1)
     bf16 = bool(L.tq_library_query(b"gemm_bf16") == 1)
     f16 = bf16 and bool(L.tq_library_query(b"gemm_f16") == 1)
-    f16_g3 = f16 and L.tq_library_query(b"gemm_f16_var") == 2   # Gauss 3M on the f16 terms
+    f16_g3 = f16 and L.tq_library_query(b"gemm_f16_var") in (2, 5)   # Gauss 3M on the f16 terms
     value = n_amp * args.steps / dt
     nl = max(1, gemm["launches"])
     avg_gemm_s = gemm["ms"] / 1e3 / nl
@@ -462,11 +474,13 @@ def main():
             "ms_per_step": sweep_["ms"],
         }
     if rank == 0:
+        _log("permute probe")
         try:
             res["permute"] = permute_probe(dev)
         except Exception as e:  # the probe must never hide the headline
             res["permute"] = {"error": repr(e)}
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        _log("cpu baseline")
         try:
             res["cpu_baseline"] = cpu_baseline(args.config)
         except Exception as e:  # the baseline must never hide the GPU number
@@ -474,11 +488,14 @@ def main():
     if world == 1 and rank == 0 and f16 and not args.no_alt:
         for key, var, desc in (("alt_bf16_split", "TQ_GEMM_F16", "bf16 3-term split, v_mfma_f32_32x32x16_bf16"),
                                ("alt_f32_mfma", "TQ_GEMM_BF16", "v_mfma_f32_32x32x2_f32")):
+            _log(f"alternate GEMM headline: {desc}")
             try:
                 res[key] = alt_gemm(args, var, desc)
             except Exception as e:  # the alternate lines must never hide the headline
                 res[key] = {"error": repr(e)}
     if not args.no_c5:   # every rank runs its share of the candidates
+        if rank == 0:
+            _log("C5 training line")
         try:
             port = int(os.environ.get("MASTER_PORT", "29500")) + 7
             c5 = c5_train(with_cpu=world == 1 and not args.no_cpu_baseline, port=port, rank=rank)

@@ -110,8 +110,14 @@ def gpu_step(target, cands, streams=None):
     return losses
 
 
-def cpu_step_sample(target_np, cands, steps):
-    """torch-CPU pairwise tensordot along the same path + autograd + the reference SGDG math."""
+def _log(msg):
+    print(f"[c5_bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_step_sample(target_np, cands, steps, budget_s=10.0):
+    """torch-CPU pairwise tensordot along the same path + autograd + the reference SGDG math:
+    up to `steps` steps of every candidate, stopping once `budget_s` seconds of work are done
+    (at least one candidate-step)."""
     from oracle.optim_ref import sgdg_step
     from tneq_qc_amd.einsum import _State
     tgt = torch.from_numpy(target_np)
@@ -122,6 +128,8 @@ def cpu_step_sample(target_np, cands, steps):
     n = 0
     for _ in range(steps):
         for expr, ps, state in items:
+            if n and time.perf_counter() - t0 > budget_s:
+                return (time.perf_counter() - t0), n
             ts = [torch.tensor(p, requires_grad=True) for p in ps]
             st = _State(expr.net)
             vals = dict(enumerate(ts))
@@ -166,11 +174,13 @@ def main():
     dev = torch.device("cuda", local)
     random.seed(rank)
     mine = list(range(rank, len(CANDIDATES), world))
+    _log(f"rank {rank}: setting up {len(mine)} candidates")
     target, cands = setup(dev, set(mine))
     streams = None if a.one_stream else [torch.cuda.Stream(dev) for _ in cands]
     for _ in range(a.warmup):
         gpu_step(target, cands, streams)
     torch.cuda.synchronize()
+    _log(f"rank {rank}: warmup done; timing {a.steps} steps")
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -216,6 +226,7 @@ def main():
         runs = []
         for th in sorted({host, min(16, host)}, reverse=True):
             torch.set_num_threads(th)
+            _log(f"cpu baseline at {th} threads")
             secs, n = cpu_step_sample(target.cpu().numpy(), cands, a.cpu_steps)
             runs.append({"value": n / secs, "cores": torch.get_num_threads(), "sample": f"{n} candidate-steps"})
         best = max(runs, key=lambda r: r["value"])

@@ -133,12 +133,15 @@ def test_contract_pair_gate_apply(T, dev):
     assert np.abs(c - ref).max() / np.abs(ref).max() < 1e-5
 
 
-@pytest.fixture(params=["f16", "f16w4", "f16g3", "f16r4", "bf16", "f32"])
+@pytest.fixture(params=["f16", "f16w4", "f16g3", "f16r4", "f16s16", "f16g3w8", "bf16", "f32"])
 def c64_kernel(request):
     """Runs a test once on each complex64 K-outer kernel: the f16 2-term split of the scaled
     operands (default tile; "f16w4": 4 waves of 64x64, "f16g3": the same with Gauss's 3M
-    product, "f16r4": the default tile on a 4-slot LDS ring with one barrier per two K-steps —
-    tq_library_set("gemm_f16_var", 1 / 2 / 3)), the bf16 3-term split kernel
+    product, "f16r4": the default tile on a 4-slot LDS ring with one barrier per two K-steps,
+    "f16s16": the default tile on v_mfma_f32_16x16x32_f16 (K-chunks of a multiple of 32; others
+    fall back to the default kernel), "f16g3w8": the default tile with Gauss's 3M product —
+    tq_library_set("gemm_f16_var", 1 / 2 / 3 / 4 / 5)), the bf16
+    3-term split kernel
     (tq_library_set("gemm_f16", 0)) and the f32-MFMA LDS-DMA kernel (tq_library_set("gemm_bf16",
     0)); restores the defaults."""
     import tneq_qc_amd._lib as _lib
@@ -148,7 +151,7 @@ def c64_kernel(request):
     p = request.param
     assert L.tq_library_set(b"gemm_bf16", 0 if p == "f32" else 1) == 0
     assert L.tq_library_set(b"gemm_f16", 1 if p.startswith("f16") else 0) == 0
-    assert L.tq_library_set(b"gemm_f16_var", {"f16w4": 1, "f16g3": 2, "f16r4": 3}.get(p, 0)) == 0
+    assert L.tq_library_set(b"gemm_f16_var", {"f16w4": 1, "f16g3": 2, "f16r4": 3, "f16s16": 4, "f16g3w8": 5}.get(p, 0)) == 0
     yield p
     for k, v in zip(keys, before):
         L.tq_library_set(k, v)
@@ -157,7 +160,8 @@ def c64_kernel(request):
 @pytest.mark.parametrize("M,N,K,B,beta", [(256, 128, 16, 1, 0.0), (256, 128, 48, 3, 0.0),
                                            (512, 256, 4096, 1, 1.0), (1024, 1024, 8192, 1, 0.0),
                                            (256, 256, 2048, 2, 0.5), (768, 384, 1024, 1, 0.0),
-                                           (128, 128, 32, 1, 0.0), (384, 256, 80, 2, 1.0)])
+                                           (128, 128, 32, 1, 0.0), (384, 256, 80, 2, 1.0),
+                                           (128, 128, 64, 1, 0.5), (256, 256, 96, 2, 0.0)])
 def test_gemm_c64_kouter_fast_path(T, dev, c64_kernel, M, N, K, B, beta):
     """complex64 with A stored K x M and B stored K x N, on both fast kernels (bf16 3-term split:
     register-staged split into a double-buffered LDS image; f32 MFMA: LDS-DMA 3-stage ring) —
