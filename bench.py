@@ -364,11 +364,13 @@ def main():
     achieved = exe_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     alg_rate = alg_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     if f16:
-        pmc_b = _profile_json("pmc_gemm_f16_r02.json", args.config)
+        pmc_b = _profile_json("pmc_gemm_f16_r03.json" if f16_g3 else "pmc_gemm_f16_r02.json", args.config)
         pmc_t = pmc_b
         kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_f16: every f32 operand scaled by a power of two "
                  "(operand max from its producer sweep) and split into 2 f16 terms, 3 term products kept, f32 "
-                 "accumulation; 4 real products per complex product)")
+                 "accumulation; " + ("Gauss's 3 real products per complex product: P1 = Ar Br, P2 = Ai Bi, "
+                                     "P3 = (Ar + Ai)(Br + Bi)" if f16_g3 else "4 real products per complex product")
+                 + ")")
         exe_def = ("executed f16 MFMA flops per launch (" + ("3 real products (Gauss) x 3 term products = 18*M*N*K"
                    if f16_g3 else "4 real products x 3 term products = 24*M*N*K") + ") / avg launch time")
     elif bf16:

@@ -34,16 +34,17 @@ static int env_flag(const char* name) {
 static std::atomic<int> g_gemm_3m{env_flag("TQ_GEMM_3M")};
 static std::atomic<int> g_gemm_bf16{env_flag("TQ_GEMM_BF16")};
 static std::atomic<int> g_gemm_f16{env_flag("TQ_GEMM_F16")};
-static int env_int(const char* name) {
+static int env_int(const char* name, int dflt = 0) {
   const char* e = getenv(name);
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : dflt;
 }
-// f16-split tile variant: 0 = 8 waves of 64 x 32 (default), 1 = 4 waves of 64 x 64, 3 = the default
-// tile on a 4-slot LDS ring (one barrier per two K-steps), 2 = 4 waves of
-// 64 x 64 with Gauss's 3-multiplication product, 4 = the default tile on v_mfma_f32_16x16x32_f16
-// (K-chunks that are a multiple of 32; others run variant 0), 5 = the default tile with Gauss's
-// product (measurements: DESIGN.md §3)
-static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR")};
+// f16-split tile variant: 0 = 8 waves of 64 x 32 with the 4-multiplication complex product,
+// 1 = 4 waves of 64 x 64, 3 = tile 0 on a 4-slot LDS ring (one barrier per two K-steps), 2 = 4
+// waves of 64 x 64 with Gauss's 3-multiplication product, 4 = tile 0 on v_mfma_f32_16x16x32_f16
+// (K-chunks that are a multiple of 32; others run variant 0), 5 (default) = tile 0 with Gauss's
+// product: 9 instead of 12 MFMAs per complex tile-step; the GEMM runs power-limited, so the
+// fewer MFMAs are time (C4 r03: 5.20 vs 5.60 ms per 4-slice launch).  Measurements: DESIGN.md §3
+static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR", 5)};
 int gemm_f16_var() { return g_gemm_f16_var.load(std::memory_order_relaxed); }
 bool gemm_3m() { return g_gemm_3m.load(std::memory_order_relaxed) != 0; }
 // The complex64 K-outer fast path runs on the bf16 matrix cores with an exact 3-term split of

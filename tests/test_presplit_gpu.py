@@ -25,12 +25,16 @@ def _lib():
 
 @pytest.fixture(autouse=True)
 def presplit_on():
-    """The pre-split path is opt-in (tq_library_set("gemm_presplit", 1) / TQ_GEMM_PRESPLIT=1)."""
+    """The pre-split path is opt-in (tq_library_set("gemm_presplit", 1) / TQ_GEMM_PRESPLIT=1) and
+    runs on the 4-multiplication f16 tile (gemm_f16_var 0; the default is the Gauss tile)."""
     L = _lib()
     prev = L.tq_library_query(b"gemm_presplit")
+    prev_var = L.tq_library_query(b"gemm_f16_var")
     assert L.tq_library_set(b"gemm_presplit", 1) == 0
+    assert L.tq_library_set(b"gemm_f16_var", 0) == 0
     yield
     L.tq_library_set(b"gemm_presplit", prev)
+    L.tq_library_set(b"gemm_f16_var", prev_var)
 
 
 def _expr(cfg, dev):
