@@ -66,8 +66,9 @@ int tq_device_synchronize(void);
  * cores with f32 accuracy; env TQ_GEMM_BF16=0 selects the f32-MFMA kernel), "gemm_f16" (1, with
  * gemm_bf16: a 2-term f16 split of the power-of-two-scaled operands, 12 MFMAs per complex
  * tile-step; 0 / env TQ_GEMM_F16=0: an exact 3-term bf16 split, 24 MFMAs), "gemm_f16_var" (f16
- * tile variant: 5 (default) = 8 waves of 64x32 with Gauss's 3-multiplication product (9 MFMAs
- * per complex tile-step), 0 = the same tile with the 4-multiplication product, 1 = 4 waves of
+ * tile variant: 6 (default) = 8 waves of 64x32 with Gauss's 3-multiplication product (9 MFMAs
+ * per complex tile-step) and 3 staging sets, 5 = the same with 2 staging sets, 0 = the 64x32
+ * tile with the 4-multiplication product, 1 = 4 waves of
  * 64x64, 2 = 4 waves of 64x64 with Gauss's product, 3 = variant 0 on a 4-slot LDS ring, one
  * barrier per two K-steps, 4 = variant 0 on v_mfma_f32_16x16x32_f16; env TQ_GEMM_F16_VAR),
  * "gemm_presplit" (0 by default, env TQ_GEMM_PRESPLIT=1, with gemm_f16_var 0: a plan's per-slice

@@ -41,10 +41,12 @@ static int env_int(const char* name, int dflt = 0) {
 // f16-split tile variant: 0 = 8 waves of 64 x 32 with the 4-multiplication complex product,
 // 1 = 4 waves of 64 x 64, 3 = tile 0 on a 4-slot LDS ring (one barrier per two K-steps), 2 = 4
 // waves of 64 x 64 with Gauss's 3-multiplication product, 4 = tile 0 on v_mfma_f32_16x16x32_f16
-// (K-chunks that are a multiple of 32; others run variant 0), 5 (default) = tile 0 with Gauss's
-// product: 9 instead of 12 MFMAs per complex tile-step; the GEMM runs power-limited, so the
-// fewer MFMAs are time (C4 r03: 5.20 vs 5.60 ms per 4-slice launch).  Measurements: DESIGN.md §3
-static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR", 5)};
+// (K-chunks that are a multiple of 32; others run variant 0), 5 = tile 0 with Gauss's product: 9
+// instead of 12 MFMAs per complex tile-step (the GEMM runs power-limited, so the fewer MFMAs are
+// time: C4 r03 5.20 vs 5.60 ms per 4-slice launch), 6 (default) = variant 5 with 3 staging sets
+// (loads two K-steps ahead), room made by the ordered term pairs (5.13 vs 5.19-5.25 ms).
+// Measurements: DESIGN.md §3
+static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR", 6)};
 int gemm_f16_var() { return g_gemm_f16_var.load(std::memory_order_relaxed); }
 bool gemm_3m() { return g_gemm_3m.load(std::memory_order_relaxed) != 0; }
 // The complex64 K-outer fast path runs on the bf16 matrix cores with an exact 3-term split of
@@ -80,7 +82,7 @@ bool gemm_configure(const char* key, int64_t v) {
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16_var") {
-    if (v < 0 || v > 5) return false;
+    if (v < 0 || v > 6) return false;
     g_gemm_f16_var = (int)v;
     return true;
   }
@@ -648,8 +650,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_, bool G3_ = false,
-          int SLOTS_ = 2>
+          int SLOTS_ = 2, bool ORD_ = false>
 struct Tile {
+  // ORD (f16, 3 term pairs): pairs in the order (l, h), (h, h), (h, l); the B-l fragments are read
+  // after the first third of the MFMAs, into the registers of the then-dead A-l fragments
+  static constexpr bool ORD = ORD_;
   // LDS slots of a K-step each: 2 = double buffer, one barrier per K-step; 4 = a ring in which a
   // step's split lands two steps ahead, one barrier per TWO K-steps
   static constexpr int SLOTS = SLOTS_;
@@ -684,6 +689,8 @@ using TileH4G = Tile<2, 2, 2, 2, 2, 3, true, true>;
 // f16, Gauss 3M on the default tile (TQ_GEMM_F16_VAR=5): 8 waves of 64 x 32, 3 x 32 accumulators,
 // 2 staging sets (power: 25 % fewer MFMAs, 50 % more LDS term planes)
 using TileH8G = Tile<2, 4, 2, 1, 2, 2, true, true>;
+// the same with 3 staging sets (loads two K-steps ahead) and the ordered term pairs (var 6)
+using TileH8G3 = Tile<2, 4, 2, 1, 2, 3, true, true, 2, true>;
 // f16, one barrier per two K-steps (TQ_GEMM_F16_VAR=3): the default tile on a 4-slot LDS ring
 using TileH2 = Tile<2, 4, 2, 1, 2, 4, true, false, 4>;
 
@@ -1023,10 +1030,14 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   typedef uint4 FragB[NGRP * NTM][TJ];
   // planes in the order the MFMA pairs first use them (pair 0's four first), so the first MFMAs
   // of a step wait for a third to a half of the step's fragment reads, not all of them
+  static_assert(!TL::ORD || SP::NPAIR == 3, "ordered pairs: the f16 split");
+  constexpr int QO[3] = {0, TL::ORD ? 2 : 1, TL::ORD ? 1 : 2};
+  auto qat = [&](int qq) { return SP::NPAIR == 3 ? QO[qq] : qq; };
   auto read_frags = [&](const char* s, FragA& fa, FragB& fb) {
     bool ra[NTM] = {}, rb[NTM] = {};
 #pragma unroll
-    for (int q = 0; q < SP::NPAIR; ++q) {
+    for (int qq = 0; qq < SP::NPAIR; ++qq) {
+      const int q = qat(qq);
       const int xa = SP::pa(q), xb = SP::pb(q);
       if (!ra[xa]) {
         ra[xa] = true;
@@ -1049,9 +1060,10 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   // pairs of (A term, B term), smallest first
   auto mfmas = [&](const FragA& fa, const FragB& fb) {
 #pragma unroll
-    for (int q = 0; q < SP::NPAIR; ++q)
+    for (int qq = 0; qq < SP::NPAIR; ++qq)
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
+        const int q = qat(qq);
         const uint4 ar = fa[SP::pa(q)][i];
         const uint4 ai = fa[NTM + SP::pa(q)][i];
         if constexpr (G3) {
@@ -1104,8 +1116,16 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       constexpr int NM = SP::NPAIR * TI * TJ * (G3 ? 3 : 4);
       constexpr int NR = NGRP * NTM * (TI + TJ);
       constexpr int NWR = 2 * NGRP * NTM;  // LDS stores per thread: 2 rows x planes
-      __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-      Interleave<0, NM, 3, (NM / NWR > 0 ? NM / NWR : 1)>::run();
+      constexpr int E = NM / NWR > 0 ? NM / NWR : 1;
+      if constexpr (TL::ORD) {
+        __builtin_amdgcn_sched_group_barrier(0x100, NR - NGRP * TJ, 0);
+        Interleave<0, NM / 3, 3, E>::run();
+        __builtin_amdgcn_sched_group_barrier(0x100, NGRP * TJ, 0);
+        Interleave<NM / 3, NM, 3, E>::run();
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        Interleave<0, NM, 3, E>::run();
+      }
     }
     __builtin_amdgcn_sched_barrier(0);  // the MFMAs of step t stay above the barrier
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1837,7 +1857,10 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.bad = ps->bad;
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitPre>), dim3((unsigned)nb),
                                dim3(xbf::TileH::NT), 0, stream, f);
-          } else if (var == 5)
+          } else if (var == 6)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8G3, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH8G3::NT), 0, stream, f);
+          else if (var == 5)
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8G, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH8G::NT), 0, stream, f);
           else if (var == 4 && f.kchunk % xbf::Tile16::BK == 0)

@@ -84,11 +84,11 @@ gg = [g for g in res["groups"] if g["family"] == "gemm_f16_split"]
 if gg:
     g = max(gg, key=lambda x: x["dispatches"])
     batch, M, N, K = 4, 1024, 1024, 65536
-    g3 = os.environ.get("TQ_GEMM_F16_VAR", "5") in ("2", "5")   # Gauss 3M: 9 MFMAs per tile-step
+    g3 = os.environ.get("TQ_GEMM_F16_VAR", "6") in ("2", "5", "6")   # Gauss 3M: 9 MFMAs per tile-step
     n_mfma = batch * (9 if g3 else 12) * (M // 32) * (N // 32) * (K // 16)
     c = g["counters_avg"]
     gem = {"config": "C4",
-           "kernel": ("gemm_c64_kouter_split_kernel<TileH8G, SplitF16> (complex64 via 2-term f16 split of the "
+           "kernel": ("gemm_c64_kouter_split_kernel<TileH8G3, SplitF16> (complex64 via 2-term f16 split of the "
                       "power-of-two-scaled operands, Gauss 3M" if g3 else
                       "gemm_c64_kouter_split_kernel<TileH, SplitF16> (complex64 via 2-term f16 split of the "
                       "power-of-two-scaled operands, 4M") +
