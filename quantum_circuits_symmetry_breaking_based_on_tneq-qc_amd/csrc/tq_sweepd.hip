@@ -67,7 +67,7 @@ constexpr int kLevels = 7;            // column-base tables: 6 column bits each,
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int TIN>
+template <int TIN, bool NTS>
 __global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
   static_assert(TIN % 2 == 0 && TIN <= kS2DMaxTin, "k-steps of 2");
   constexpr int KS = TIN / 2;
@@ -151,7 +151,8 @@ __global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
         const f2v a = f16_terms(f2v{w.x, w.y}, sc), b = f16_terms(f2v{w.z, w.w}, sc);
         w = f4v{a.x, a.y, b.x, b.y};
       }
-      if (op.pad != 2) *p = w;   // development diagnostic (TQ_S2D_DIAG=2): no stores
+      if constexpr (NTS) __builtin_nontemporal_store(w, p);   // streaming stores (TQ_S2D_NT=1)
+      else if (op.pad != 2) *p = w;   // development diagnostic (TQ_S2D_DIAG=2): no stores
       else if (w.x == 12345.f) *p = w;
     }
   };
@@ -215,16 +216,23 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
   }
   // one round of resident workgroups over the launch's ops (the kernel strides over its tiles):
   // a second, partial round of workgroups left most CUs idle (1024 blocks on 768 slots)
+  static const bool nts = [] {
+    const char* e = getenv("TQ_S2D_NT");
+    return e && e[0] == '1';
+  }();
   const void* fn = nullptr;
+#define TQ_SD_FN(T) (nts ? reinterpret_cast<const void*>(&sweepd_kernel<T, true>) \
+                         : reinterpret_cast<const void*>(&sweepd_kernel<T, false>))
   switch (tin) {
-    case 2: fn = reinterpret_cast<const void*>(&sweepd_kernel<2>); break;
-    case 4: fn = reinterpret_cast<const void*>(&sweepd_kernel<4>); break;
-    case 8: fn = reinterpret_cast<const void*>(&sweepd_kernel<8>); break;
-    case 16: fn = reinterpret_cast<const void*>(&sweepd_kernel<16>); break;
+    case 2: fn = TQ_SD_FN(2); break;
+    case 4: fn = TQ_SD_FN(4); break;
+    case 8: fn = TQ_SD_FN(8); break;
+    case 16: fn = TQ_SD_FN(16); break;
     default:
       set_error("sweepd: tin must be 2, 4, 8 or 16");
       return TQ_ERR_INVALID;
   }
+#undef TQ_SD_FN
   static int slots[kS2DMaxTin + 1] = {};
   if (!slots[tin]) {
     int dev = 0, cus = 0, per = 0;
@@ -246,12 +254,8 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     R.op[q].pad = diag;
     blocks += R.op[q].nblocks;
   }
-  switch (tin) {
-    case 2: hipLaunchKernelGGL(sweepd_kernel<2>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
-    case 4: hipLaunchKernelGGL(sweepd_kernel<4>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
-    case 8: hipLaunchKernelGGL(sweepd_kernel<8>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
-    default: hipLaunchKernelGGL(sweepd_kernel<16>, dim3(blocks), dim3(64 * kWaves), 0, stream, R); break;
-  }
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(S2DLaunch)>(const_cast<void*>(fn)), dim3(blocks), dim3(64 * kWaves), 0,
+                     stream, R);
   TQ_HIP(hipGetLastError());
   return TQ_OK;
 }
