@@ -82,7 +82,7 @@ bool gemm_configure(const char* key, int64_t v) {
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16_var") {
-    if (v < 0 || v > 6) return false;
+    if (v < 0 || v > 8) return false;
     g_gemm_f16_var = (int)v;
     return true;
   }
@@ -650,8 +650,15 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_, bool G3_ = false,
-          int SLOTS_ = 2, bool ORD_ = false>
+          int SLOTS_ = 2, bool ORD_ = false, bool POUT_ = false, bool STG_ = false>
 struct Tile {
+  // STG (with POUT): a K-step's fragments are read one product group (re / im / re+im planes) at
+  // a time, group h+1's under group h's MFMAs: two groups' fragments live instead of three
+  static constexpr bool STG = STG_;
+  // POUT (Gauss 3M): MFMAs ordered product-major -- the three term products of one real product
+  // back to back on one accumulator, so consecutive MFMAs share an operand (A-l B-h, A-h B-h,
+  // A-h B-l) instead of changing both
+  static constexpr bool POUT = POUT_;
   // ORD (f16, 3 term pairs): pairs in the order (l, h), (h, h), (h, l); the B-l fragments are read
   // after the first third of the MFMAs, into the registers of the then-dead A-l fragments
   static constexpr bool ORD = ORD_;
@@ -691,6 +698,10 @@ using TileH4G = Tile<2, 2, 2, 2, 2, 3, true, true>;
 using TileH8G = Tile<2, 4, 2, 1, 2, 2, true, true>;
 // the same with 3 staging sets (loads two K-steps ahead) and the ordered term pairs (var 6)
 using TileH8G3 = Tile<2, 4, 2, 1, 2, 3, true, true, 2, true>;
+// variant 5 with product-major MFMA order (var 7)
+using TileH8GP = Tile<2, 4, 2, 1, 2, 2, true, true, 2, false, true>;
+// product-major order, fragments read per product group, 3 staging sets (var 8)
+using TileH8GS = Tile<2, 4, 2, 1, 2, 3, true, true, 2, false, true, true>;
 // f16, one barrier per two K-steps (TQ_GEMM_F16_VAR=3): the default tile on a 4-slot LDS ring
 using TileH2 = Tile<2, 4, 2, 1, 2, 4, true, false, 4>;
 
@@ -1058,7 +1069,45 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
     }
   };
   // pairs of (A term, B term), smallest first
+  // one product group's fragments (planes h * NTM + term of A and B) / MFMAs (TL::STG)
+  auto read_group = [&](const char* s, int h, FragA& fa, FragB& fb) {
+#pragma unroll
+    for (int x = 0; x < NTM; ++x) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        fa[h * NTM + x][i] = *reinterpret_cast<const uint4*>(s + (h * NTM + x) * SUBA + a_off[i]);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        fb[h * NTM + x][j] = *reinterpret_cast<const uint4*>(s + (h * NTM + x) * SUBB + b_off[j]);
+    }
+  };
+  auto mfma_group = [&](int h, const FragA& fa, const FragB& fb) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int qq = 0; qq < SP::NPAIR; ++qq) {
+          const int q = qat(qq);
+          acc[h][i][j] = SP::mfma(fa[h * NTM + SP::pa(q)][i], fb[h * NTM + SP::pb(q)][j], acc[h][i][j]);
+        }
+  };
   auto mfmas = [&](const FragA& fa, const FragB& fb) {
+    if constexpr (TL::POUT) {
+      static_assert(G3 && SP::NPAIR == 3, "product-major order: Gauss 3M on the f16 split");
+#pragma unroll
+      for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int qq = 0; qq < 3; ++qq) {
+              const int q = qat(qq);
+              acc[h][i][j] = SP::mfma(fa[h * NTM + SP::pa(q)][i], fb[h * NTM + SP::pb(q)][j], acc[h][i][j]);
+            }
+      return;
+    }
 #pragma unroll
     for (int qq = 0; qq < SP::NPAIR; ++qq)
 #pragma unroll
@@ -1106,6 +1155,29 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
     constexpr int P = decltype(par)::value;
     load(std::integral_constant<int, P % NSET>{}, t + NSET < nkt ? t + NSET : nkt - 1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (TL::STG) {
+      static_assert(TL::POUT && TL::ILV, "staged group reads: product-major, interleaved");
+      const char* sb = lds + (P & 1) * BUF;
+      read_group(sb, 0, fa, fb);
+      store_stage(std::integral_constant<int, (P + 1) % NSET>{}, (P & 1) ^ 1);
+      read_group(sb, 1, fa, fb);
+      mfma_group(0, fa, fb);
+      read_group(sb, 2, fa, fb);
+      mfma_group(1, fa, fb);
+      mfma_group(2, fa, fb);
+      constexpr int NMG = SP::NPAIR * TI * TJ;      // MFMAs per product group
+      constexpr int NRG = NTM * (TI + TJ);          // fragment reads per product group
+      constexpr int NWR = 2 * NGRP * NTM;
+      constexpr int E = 3 * NMG / NWR > 0 ? 3 * NMG / NWR : 1;
+      __builtin_amdgcn_sched_group_barrier(0x100, NRG, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, NRG, 0);
+      Interleave<0, NMG, 3, E>::run();
+      __builtin_amdgcn_sched_group_barrier(0x100, NRG, 0);
+      Interleave<NMG, 3 * NMG, 3, E>::run();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      return;
+    }
     read_frags(lds + (P & 1) * BUF, fa, fb);
     store_stage(std::integral_constant<int, (P + 1) % NSET>{}, (P & 1) ^ 1);
     mfmas(fa, fb);
@@ -1857,7 +1929,13 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.bad = ps->bad;
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitPre>), dim3((unsigned)nb),
                                dim3(xbf::TileH::NT), 0, stream, f);
-          } else if (var == 6)
+          } else if (var == 8)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8GS, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH8GS::NT), 0, stream, f);
+          else if (var == 7)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8GP, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH8GP::NT), 0, stream, f);
+          else if (var == 6)
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8G3, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH8G3::NT), 0, stream, f);
           else if (var == 5)
