@@ -149,6 +149,15 @@ bool fast_disabled() {
   return v != 0;
 }
 
+// TQ_GEMM_SKINNY=0 sends the M * N <= 16 contractions to the tiled kernels (A/B timing)
+bool skinny_disabled() {
+  static const int v = [] {
+    const char* e = getenv("TQ_GEMM_SKINNY");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 template <typename R>
 __device__ __forceinline__ void mfma(R a, R b, typename std::conditional<sizeof(R) == 4, f32x16, f64x4>::type& c);
 template <>
@@ -1857,6 +1866,142 @@ splitk_reduce_kernel(const R* __restrict__ W, R* __restrict__ C, int64_t M, int6
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skinny contraction: C (M x N with M * N <= 16, M and N powers of two) = op(A) op(B) over a
+// long K -- the gradient steps of the reverse-mode tree (a gate's 4 x 4 / 8 x 2 / 2 x 8 gradient
+// contracted over 2^6-2^14 elements of the running tensor: ~250 of them per C5 training step,
+// engine_siamese.py:351-554 / symmetry_breaking_quantum.py:210-224), where a 64 x 64 MFMA tile
+// would be 1/256 used and split 64 ways over K.  A block sums a K-range into per-thread registers
+// (one k per thread per iteration, all M * N products), reduces across its waves and writes one
+// partial (or C itself when it is the only block); skinny_reduce_kernel sums the partials in a
+// fixed order and applies beta.  Element strides make every transposition one kernel.
+template <typename R, bool CPLX, int SM, int SN>
+__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs g, int64_t sam, int64_t sak,
+                                                         int64_t sbk, int64_t sbn, int P) {
+  constexpr int EW = CPLX ? 2 : 1, MN = SM * SN, NW = 256 / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int p = blockIdx.x;
+  const int64_t b = blockIdx.y;
+  const int64_t kc = (g.K + P - 1) / P;
+  const int64_t k0 = (int64_t)p * kc, k1 = k0 + kc < g.K ? k0 + kc : g.K;
+  const R* A = reinterpret_cast<const R*>(g.A) + b * g.sA * EW;
+  const R* B = reinterpret_cast<const R*>(g.B) + b * g.sB * EW;
+  R cr[MN], ci[MN];
+#pragma unroll
+  for (int e = 0; e < MN; ++e) cr[e] = ci[e] = R(0);
+  for (int64_t k = k0 + tid; k < k1; k += 256) {
+    R ar[SM], ai[SM], br[SN], bi[SN];
+#pragma unroll
+    for (int m = 0; m < SM; ++m) {
+      const R* q = A + (m * sam + k * sak) * EW;
+      ar[m] = q[0];
+      ai[m] = CPLX ? q[1] : R(0);
+    }
+#pragma unroll
+    for (int n = 0; n < SN; ++n) {
+      const R* q = B + (k * sbk + n * sbn) * EW;
+      br[n] = q[0];
+      bi[n] = CPLX ? q[1] : R(0);
+    }
+#pragma unroll
+    for (int m = 0; m < SM; ++m)
+#pragma unroll
+      for (int n = 0; n < SN; ++n) {
+        cr[m * SN + n] += ar[m] * br[n];
+        if constexpr (CPLX) {
+          cr[m * SN + n] -= ai[m] * bi[n];
+          ci[m * SN + n] += ar[m] * bi[n] + ai[m] * br[n];
+        }
+      }
+  }
+#pragma unroll
+  for (int e = 0; e < MN; ++e)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cr[e] += __shfl_xor(cr[e], o);
+      if constexpr (CPLX) ci[e] += __shfl_xor(ci[e], o);
+    }
+  __shared__ R red[NW][MN * EW];
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < MN; ++e) {
+      red[wv][e * EW] = cr[e];
+      if constexpr (CPLX) red[wv][e * EW + 1] = ci[e];
+    }
+  }
+  __syncthreads();
+  if (tid < MN * EW) {
+    R v = red[0][tid];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w][tid];
+    if (P > 1) {
+      reinterpret_cast<R*>(g.W)[((int64_t)p * g.batch + b) * MN * EW + tid] = v;
+    } else {
+      const int e = tid / EW, c = tid % EW;
+      R* cp = reinterpret_cast<R*>(g.C) + (b * g.sC + (int64_t)(e / SN) * g.ldc + (e % SN)) * EW + c;
+      *cp = g.beta != 0.0 ? v + (R)g.beta * *cp : v;
+    }
+  }
+}
+
+// C_b = sum_p W[p][b] + beta * C_b for the skinny kernel's partials (fixed summation order)
+template <typename R>
+__global__ void __launch_bounds__(64) skinny_reduce_kernel(const R* __restrict__ W, R* __restrict__ C,
+                                                          int64_t N, int64_t ldc, int64_t sC,
+                                                          int64_t batch, int P, int mne, int ew, double beta) {
+  const int e = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  if (e >= mne) return;
+  R s[8] = {};
+  int p = 0;
+  for (; p + 8 <= P; p += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += W[((int64_t)(p + u) * batch + b) * mne + e];
+  }
+  for (; p < P; ++p) s[0] += W[((int64_t)p * batch + b) * mne + e];
+  R v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  const int el = e / ew, c = e % ew;
+  R* cp = C + (b * sC + (int64_t)(el / N) * ldc + (el % N)) * ew + c;
+  *cp = beta != 0.0 ? v + (R)beta * *cp : v;
+}
+
+// the skinny path for M * N <= 16 (M, N powers of two): launched here (TQ_OK or a launch error);
+// 1 when the shape is not one of its shapes
+template <typename R, bool CPLX>
+int launch_skinny(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_t batch,
+                  const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB,
+                  double beta, void* C, int64_t ldc, int64_t sC, void* W, size_t wsb, hipStream_t stream) {
+  auto p2 = [](int64_t v) { return v >= 1 && v <= 16 && (v & (v - 1)) == 0; };
+  if (!p2(M) || !p2(N) || M * N > 16 || K < 64 || batch > 65535 || skinny_disabled()) return 1;
+  constexpr int EW = CPLX ? 2 : 1;
+  // ~2048 k per block (8 per thread); the partials must fit the workspace
+  int P = (int)std::min<int64_t>(64, std::max<int64_t>(1, (K + 2047) / 2048));
+  const size_t per = (size_t)batch * M * N * EW * sizeof(R);
+  if (P > 1 && (W == nullptr || wsb < (size_t)P * per)) P = W ? (int)std::max<size_t>(1, std::min<size_t>(P, wsb / per)) : 1;
+  GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.W = W;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.sA = sA; g.sB = sB; g.sC = sC; g.batch = batch; g.beta = beta;
+  const int64_t sam = transA ? 1 : lda, sak = transA ? lda : 1;
+  const int64_t sbk = transB ? 1 : ldb, sbn = transB ? ldb : 1;
+  const dim3 grid((unsigned)P, (unsigned)batch);
+#define TQ_SK(m, n) \
+  if (M == m && N == n) hipLaunchKernelGGL((gemm_skinny_kernel<R, CPLX, m, n>), grid, dim3(256), 0, stream, g, sam, sak, sbk, sbn, P);
+  TQ_SK(1, 1) TQ_SK(1, 2) TQ_SK(1, 4) TQ_SK(1, 8) TQ_SK(1, 16)
+  TQ_SK(2, 1) TQ_SK(2, 2) TQ_SK(2, 4) TQ_SK(2, 8)
+  TQ_SK(4, 1) TQ_SK(4, 2) TQ_SK(4, 4)
+  TQ_SK(8, 1) TQ_SK(8, 2)
+  TQ_SK(16, 1)
+#undef TQ_SK
+  TQ_HIP(hipGetLastError());
+  if (P > 1) {
+    hipLaunchKernelGGL((skinny_reduce_kernel<R>), dim3((unsigned)batch), dim3(64), 0, stream, (const R*)W, (R*)C,
+                       N, ldc, sC, batch, P, (int)(M * N * EW), EW, beta);
+    TQ_HIP(hipGetLastError());
+  }
+  return TQ_OK;
+}
+
 template <typename R> int ew_of(int dtype) { return dtype_complex(dtype) ? 2 : 1; }
 
 int choose_splits(int64_t tiles, int64_t K, int BK) {
@@ -2027,6 +2172,10 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       return TQ_OK;
     }
   }
+  if (const int rc = launch_skinny<R, CPLX>(transA, transB, M, N, K, batch, A, lda, sA, B, ldb, sB, beta, C, ldc,
+                                            sC, W, wsb, stream);
+      rc != 1)
+    return rc;
   GemmArgs g{};
   g.A = A; g.B = B; g.C = C; g.W = W;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;

@@ -277,3 +277,27 @@ def test_gemm_c64_batched_entry_scales(T, dev, c64_kernel):
     for i in range(B):
         err = np.abs(c[i] - ref[i]).max() / np.abs(ref[i]).max()
         assert err < TOL["complex64"], (i, err)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,K,B,beta", [(4, 4, 16384, 1, 0.0), (8, 2, 8192, 2, 0.5), (2, 8, 512, 1, 1.0),
+                                           (1, 1, 100, 3, 0.0), (16, 1, 3000, 1, 0.0), (4, 4, 64, 2, 0.0),
+                                           (1, 16, 70000, 1, 0.0)])
+def test_gemm_skinny(T, dev, dt, M, N, K, B, beta):
+    """The skinny contraction path (M * N <= 16, M and N powers of two, long K: the reverse-mode
+    gradient steps of the C5 training loop) in all four transpositions, batched, with beta, K
+    not a multiple of the block range, against the exact product."""
+    import tneq_qc_amd.ops as ops
+    rng = np.random.default_rng(K + M)
+    for ta, tb in itertools.product((False, True), (False, True)):
+        a = _rand(rng, (B, K, M) if ta else (B, M, K), dt)
+        b = _rand(rng, (B, N, K) if tb else (B, K, N), dt)
+        c0 = _rand(rng, (B, M, N), dt)
+        cd = _to(T, dev, c0)
+        ops.gemm(_to(T, dev, a), _to(T, dev, b), ta, tb, out=cd, beta=beta)
+        hi = "complex128" if dt.startswith("complex") else "float64"
+        aa = np.swapaxes(a, 1, 2) if ta else a
+        bb = np.swapaxes(b, 1, 2) if tb else b
+        ref = np.matmul(aa.astype(hi), bb.astype(hi)) + beta * c0.astype(hi)
+        err = np.abs(cd.cpu().numpy() - ref).max() / np.abs(ref).max()
+        assert err < TOL[dt], (ta, tb, err)
