@@ -208,8 +208,10 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
            "amplitudes_per_forward": d["amplitudes_per_forward"],
            "host_issue_ms_per_step": d.get("host_issue_ms_per_step"),
            "wall_ms_per_step_per_rank": d.get("wall_ms_per_step_per_rank"),
-           "bound": "latency / host issue (2^16-element tensors; ~100 dependent pairwise launches per "
-                    "candidate-step; a rank's candidates overlap on their own streams)"}
+           "step_graphs": d.get("step_graphs"),
+           "bound": "latency (2^16-element tensors; ~100 dependent pairwise launches per candidate-step, "
+                    "forward + loss + backward replayed as one hipGraph per candidate, SGDG eager; a rank's "
+                    "candidates overlap on their own streams)"}
     if "cpu_baseline" in d:
         out["cpu_baseline"] = dict(d["cpu_baseline"], cpu_model=_cpu_model())
     return out

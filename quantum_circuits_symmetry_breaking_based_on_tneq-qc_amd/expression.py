@@ -410,7 +410,12 @@ class _TreeRuntime:
                 pl.execute(ptrs, self.h[a].data_ptr(), stream)
 
     def _run(self, kind, key, fn):
-        """fn() eagerly; captured into a graph the second time `key` is seen, replayed after."""
+        """fn() eagerly; captured into a graph the second time `key` is seen, replayed after.
+        Inside a caller's capture (a whole training step being captured, graphs.capture_step)
+        the launches go straight into that capture."""
+        if torch.cuda.is_current_stream_capturing():
+            fn()
+            return
         g = self.graphs.get(key)
         if g is not None:
             g.replay()

@@ -42,6 +42,7 @@ from tneq_qc_amd.circuits import BrickWall, TRAIN_MASK  # noqa: E402
 from tneq_qc_amd.contractor import EinsumStrategy  # noqa: E402
 from tneq_qc_amd.einsum import parse_equation, partition_path  # noqa: E402
 from tneq_qc_amd.expression import HipContractExpression  # noqa: E402
+from tneq_qc_amd.graphs import capture_step  # noqa: E402
 from tneq_qc_amd.optim import SGDG  # noqa: E402
 
 N_Q, DEPTH = 8, 10
@@ -86,10 +87,24 @@ def fidelity_loss(out, tgt):
     return 1.0 - num / den
 
 
-def gpu_step(target, cands, streams=None):
+def capture(target, cands, dev):
+    """Each candidate's forward + fidelity loss + backward as one hipGraph (graphs.capture_step):
+    a step then replays it and runs SGDG eagerly (the host-side retraction draw stays per step)."""
+    graphs = []
+    for (expr, params, _, _, _, _) in cands:
+        def fb(expr=expr, params=params):
+            loss = fidelity_loss(expr(*params), target)
+            loss.backward()
+            return loss
+        graphs.append(capture_step(fb, params, dev))
+    return graphs
+
+
+def gpu_step(target, cands, streams=None, graphs=None):
     """One training step of every candidate.  With `streams`, candidate k runs on streams[k]: the
     candidates are independent fits, so their latency-bound launch chains (each plan replays its
-    own hipGraphs) overlap on the GPU instead of queueing behind each other."""
+    own hipGraphs) overlap on the GPU instead of queueing behind each other.  With `graphs`
+    (capture()), forward + loss + backward of candidate k is one graph replay."""
     losses = []
     cur = torch.cuda.current_stream()
     for k, (expr, params, opt, _, _, rstate) in enumerate(cands):
@@ -97,9 +112,13 @@ def gpu_step(target, cands, streams=None):
         if streams:
             st.wait_stream(cur)
         with torch.cuda.stream(st):
-            opt.zero_grad()
-            loss = fidelity_loss(expr(*params), target)
-            loss.backward()
+            if graphs is not None:
+                g, loss = graphs[k]
+                g.replay()
+            else:
+                opt.zero_grad()
+                loss = fidelity_loss(expr(*params), target)
+                loss.backward()
             random.setstate(rstate[0])
             opt.step()
             rstate[0] = random.getstate()
@@ -161,6 +180,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--one-stream", action="store_true", help="candidates one after another on one stream")
+    ap.add_argument("--eager", action="store_true",
+                    help="forward / loss / backward issued eagerly every step (default: one hipGraph per candidate)")
     ap.add_argument("--port", type=int, default=0, help="gloo timing group port (multi-rank)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -177,15 +198,16 @@ def main():
     _log(f"rank {rank}: setting up {len(mine)} candidates")
     target, cands = setup(dev, set(mine))
     streams = None if a.one_stream else [torch.cuda.Stream(dev) for _ in cands]
+    graphs = None if a.eager else capture(target, cands, dev)
     for _ in range(a.warmup):
-        gpu_step(target, cands, streams)
+        gpu_step(target, cands, streams, graphs)
     torch.cuda.synchronize()
     _log(f"rank {rank}: warmup done; timing {a.steps} steps")
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        losses = gpu_step(target, cands, streams)
+        losses = gpu_step(target, cands, streams, graphs)
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     dt_local = time.perf_counter() - t0
@@ -211,6 +233,7 @@ def main():
            "candidates_per_rank": [len(range(r, len(CANDIDATES), world)) for r in range(world)],
            "cores_per_candidate": len(cands[0][1]), "dtype": "c128",
            "streams": len(streams) if streams else 1,
+           "step_graphs": graphs is not None,
            "forward": "QCTN.split halves swept + boundary contraction (split/merge path), one native plan",
            "amplitudes_per_forward": int(np.prod(cands[0][0].out_shape)),
            "host_issue_ms_per_step": [float(t[2]) / a.steps * 1e3 for t in allt],

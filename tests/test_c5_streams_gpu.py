@@ -40,3 +40,29 @@ def test_candidates_on_streams_equal_sequential(dev):
     for ca, cb_ in zip(p0, p1):
         for a, b in zip(ca, cb_):
             assert (a - b).abs().max().item() <= 1e-12 * max(1.0, a.abs().max().item())
+
+
+def test_graphed_steps_equal_eager(dev):
+    """Forward + loss + backward of every candidate captured once as a hipGraph
+    (tneq_qc_amd.graphs.capture_step) and replayed per step, SGDG eager: the same losses and
+    parameters as the eager steps (complex128, <= 1e-12 relative), candidates on streams."""
+    import torch
+    cb = _c5()
+    runs = []
+    for graphed in (False, True):
+        random.seed(0)
+        target, cands = cb.setup(dev)
+        streams = [torch.cuda.Stream(dev) for _ in cands]
+        graphs = cb.capture(target, cands, dev) if graphed else None
+        losses = []
+        for _ in range(3):
+            losses.append([float(l.detach()) for l in cb.gpu_step(target, cands, streams, graphs)])
+        torch.cuda.synchronize()
+        runs.append((losses, [[p.detach().clone() for p in c[1]] for c in cands]))
+    (l0, p0), (l1, p1) = runs
+    for a, b in zip(l0, l1):
+        for x, y in zip(a, b):
+            assert abs(x - y) <= 1e-12 * max(1.0, abs(x))
+    for ca, cb_ in zip(p0, p1):
+        for a, b in zip(ca, cb_):
+            assert (a - b).abs().max().item() <= 1e-12 * max(1.0, a.abs().max().item())
