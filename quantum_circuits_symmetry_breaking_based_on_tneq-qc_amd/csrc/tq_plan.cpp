@@ -1199,7 +1199,14 @@ class Compiler {
     // the positions it adds are not live before it, so input k sits in slot r0 + k.
     // register blocks of consecutive square gates (S2Desc::pmeta): the pass starting at gate j
     // ends before block_span(j, ng); bm = its block positions, live = the live positions
-    const int B = s2_block_bits((int)P_.esz, int64_t(1) << (lc + used));
+    // TQ_S2_B4MIN: the smallest tile (elements) that gets 16-element register blocks (default
+    // 8192: every thread busy; smaller tiles leave threads idle in the block passes)
+    static const int64_t b4min = [] {
+      const char* e = getenv("TQ_S2_B4MIN");
+      return e ? (int64_t)atoll(e) : (int64_t)8192;
+    }();
+    const int64_t tile_elems = int64_t(1) << (lc + used);
+    const int B = (P_.esz <= 8 && tile_elems >= b4min) ? 4 : s2_block_bits((int)P_.esz, tile_elems);
     auto kmask_of = [&](int j) {
       uint32_t m = 0;
       for (int k = 0; k < d.gate[j].K; ++k) m |= (uint32_t)kdep[j][k];

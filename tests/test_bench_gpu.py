@@ -36,3 +36,17 @@ def test_bench_two_ranks_self_launch(tmp_path):
     assert a.shape == b.shape == (2,) * 20
     err = np.abs(a - b).max() / np.abs(a).max()
     assert err < 2e-5, err
+
+
+@pytest.mark.timeout(900)
+def test_bench_eight_ranks_one_slice_each(tmp_path):
+    """The N = 8 layout of the driver's scaling run rehearsed on one GPU: eight self-launched
+    ranks (gloo), one slice each (no slice lanes: the batch-1 split-K GEMM path), one all-reduce
+    of eight partial amplitude buffers -- equal to the 1-rank amplitudes."""
+    one = _run(["--gpus", "1"], str(tmp_path / "one.npy"))
+    eight = _run(["--gpus", "8", "--devices", "0,0,0,0,0,0,0,0", "--dist-backend", "gloo"],
+                 str(tmp_path / "eight.npy"))
+    assert eight["n_gpus"] == 8 and eight["config"]["slices_per_rank"] == 1
+    a, b = np.load(tmp_path / "one.npy"), np.load(tmp_path / "eight.npy")
+    err = np.abs(a - b).max() / np.abs(a).max()
+    assert err < 2e-5, err
