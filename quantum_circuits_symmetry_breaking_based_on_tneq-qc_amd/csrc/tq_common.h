@@ -122,6 +122,26 @@ int presplit_prep_launch(uint32_t* amax, int32_t* sc, int n, hipStream_t stream)
 // word for the whole batch; plan slice lanes: n_amax_slice, every lane scaled by its own max).
 // Without the words the pre-pass keeps one max per batch entry and operand.
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
+// Strided skinny contraction (tq_gemm.hip): C[m][n] (M x N contiguous, M * N <= 16, M, N powers
+// of two) = sum_k A(m, k) B(k, n) where every index is a bit string of power-of-two modes read
+// through per-bit element strides (w*), so no operand is permuted first -- the gradient steps of
+// a reverse-mode tree (a gate's gradient against a large tensor in any mode order).
+constexpr int kSkMaxKBits = 24;
+struct SkinnyArgs {
+  const void* A = nullptr;
+  const void* B = nullptr;
+  void* C = nullptr;
+  void* W = nullptr;            // partials (P x M x N elements) when P > 1
+  int64_t K = 0;
+  int nkb = 0;                  // K = 2^nkb
+  int M = 1, N = 1;
+  double beta = 0;
+  int64_t wam[4] = {}, wbn[4] = {};                     // bit b of m / n
+  int64_t wak[kSkMaxKBits] = {}, wbk[kSkMaxKBits] = {}; // bit b of k
+};
+// partial blocks of a strided skinny contraction over K (its workspace = P x M x N elements)
+int skinny_blocks(int64_t K);
+int skinny_strided_launch(int dtype, const SkinnyArgs& a, hipStream_t stream);
 // apply a small operand along (at most two runs of) contracted modes (tq_apply.hip):
 //   C[o][n][m][i] = sum_{k1,k2} S[o][k1][m][k2][i] * G[k1*K2+k2][n]   (S, C, G contiguous)
 int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_t I, int64_t N,

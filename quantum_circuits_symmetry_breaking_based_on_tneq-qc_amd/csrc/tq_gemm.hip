@@ -2002,6 +2002,129 @@ int launch_skinny(int transA, int transB, int64_t M, int64_t N, int64_t K, int64
   return TQ_OK;
 }
 
+// The strided form (SkinnyArgs): the same sums, each operand index a bit string read through
+// per-bit element strides -- one thread's k keeps its low 8 bits (its lane id) for the whole
+// range, so those weights are summed once and the higher bits per 256-k step, wave-uniform.
+template <typename R, bool CPLX, int SM, int SN>
+__global__ void __launch_bounds__(256) gemm_skinny_strided_kernel(SkinnyArgs a, int P, int64_t kc) {
+  constexpr int EW = CPLX ? 2 : 1, MN = SM * SN, NW = 256 / 64;
+  constexpr int MB = SM == 16 ? 4 : SM == 8 ? 3 : SM == 4 ? 2 : SM == 2 ? 1 : 0;
+  constexpr int NB = SN == 16 ? 4 : SN == 8 ? 3 : SN == 4 ? 2 : SN == 2 ? 1 : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int p = blockIdx.x;
+  const int64_t k0 = (int64_t)p * kc, k1 = k0 + kc < a.K ? k0 + kc : a.K;
+  int64_t loA = 0, loB = 0;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    if (b < a.nkb && ((tid >> b) & 1)) { loA += a.wak[b]; loB += a.wbk[b]; }
+  int64_t oa[SM], ob[SN];
+#pragma unroll
+  for (int m = 0; m < SM; ++m) {
+    oa[m] = 0;
+#pragma unroll
+    for (int b = 0; b < MB; ++b) if ((m >> b) & 1) oa[m] += a.wam[b];
+  }
+#pragma unroll
+  for (int n = 0; n < SN; ++n) {
+    ob[n] = 0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) if ((n >> b) & 1) ob[n] += a.wbn[b];
+  }
+  const R* A = reinterpret_cast<const R*>(a.A);
+  const R* B = reinterpret_cast<const R*>(a.B);
+  R cr[MN], ci[MN];
+#pragma unroll
+  for (int e = 0; e < MN; ++e) cr[e] = ci[e] = R(0);
+  for (int64_t kb = k0; kb < k1; kb += 256) {
+    int64_t hiA = 0, hiB = 0;
+    const int64_t h = kb >> 8;   // kc and k0 are multiples of 256: bits >= 8 are uniform
+    for (int b = 8; b < a.nkb; ++b)
+      if ((h >> (b - 8)) & 1) { hiA += a.wak[b]; hiB += a.wbk[b]; }
+    if (kb + tid < k1) {
+      const R* pa = A + (loA + hiA) * EW;
+      const R* pb = B + (loB + hiB) * EW;
+      R ar[SM], ai[SM], br[SN], bi[SN];
+#pragma unroll
+      for (int m = 0; m < SM; ++m) {
+        ar[m] = pa[oa[m] * EW];
+        ai[m] = CPLX ? pa[oa[m] * EW + 1] : R(0);
+      }
+#pragma unroll
+      for (int n = 0; n < SN; ++n) {
+        br[n] = pb[ob[n] * EW];
+        bi[n] = CPLX ? pb[ob[n] * EW + 1] : R(0);
+      }
+#pragma unroll
+      for (int m = 0; m < SM; ++m)
+#pragma unroll
+        for (int n = 0; n < SN; ++n) {
+          cr[m * SN + n] += ar[m] * br[n];
+          if constexpr (CPLX) {
+            cr[m * SN + n] -= ai[m] * bi[n];
+            ci[m * SN + n] += ar[m] * bi[n] + ai[m] * br[n];
+          }
+        }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < MN; ++e)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cr[e] += __shfl_xor(cr[e], o);
+      if constexpr (CPLX) ci[e] += __shfl_xor(ci[e], o);
+    }
+  __shared__ R red[NW][MN * EW];
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < MN; ++e) {
+      red[wv][e * EW] = cr[e];
+      if constexpr (CPLX) red[wv][e * EW + 1] = ci[e];
+    }
+  }
+  __syncthreads();
+  if (tid < MN * EW) {
+    R v = red[0][tid];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w][tid];
+    if (P > 1) {
+      reinterpret_cast<R*>(a.W)[(int64_t)p * MN * EW + tid] = v;
+    } else {
+      R* cp = reinterpret_cast<R*>(a.C) + tid;
+      *cp = a.beta != 0.0 ? v + (R)a.beta * *cp : v;
+    }
+  }
+}
+
+template <typename R, bool CPLX>
+int skinny_strided_typed(const SkinnyArgs& a, hipStream_t stream) {
+  constexpr int EW = CPLX ? 2 : 1;
+  const int P = skinny_blocks(a.K);
+  const int64_t kc = ((a.K + P - 1) / P + 255) / 256 * 256;
+  bool hit = false;
+#define TQ_SKS(m, n)                                                                                   \
+  if (a.M == m && a.N == n) {                                                                          \
+    hipLaunchKernelGGL((gemm_skinny_strided_kernel<R, CPLX, m, n>), dim3((unsigned)P), dim3(256), 0, stream, a, P, kc); \
+    hit = true;                                                                                        \
+  }
+  TQ_SKS(1, 1) TQ_SKS(1, 2) TQ_SKS(1, 4) TQ_SKS(1, 8) TQ_SKS(1, 16)
+  TQ_SKS(2, 1) TQ_SKS(2, 2) TQ_SKS(2, 4) TQ_SKS(2, 8)
+  TQ_SKS(4, 1) TQ_SKS(4, 2) TQ_SKS(4, 4)
+  TQ_SKS(8, 1) TQ_SKS(8, 2)
+  TQ_SKS(16, 1)
+#undef TQ_SKS
+  if (!hit) {
+    set_error("skinny: M x N must be powers of two with M * N <= 16");
+    return TQ_ERR_INVALID;
+  }
+  TQ_HIP(hipGetLastError());
+  if (P > 1) {
+    hipLaunchKernelGGL((skinny_reduce_kernel<R>), dim3(1), dim3(64), 0, stream, (const R*)a.W, (R*)a.C,
+                       (int64_t)a.N, (int64_t)a.N, (int64_t)a.M * a.N, (int64_t)1, P, a.M * a.N * EW, EW, a.beta);
+    TQ_HIP(hipGetLastError());
+  }
+  return TQ_OK;
+}
+
 template <typename R> int ew_of(int dtype) { return dtype_complex(dtype) ? 2 : 1; }
 
 int choose_splits(int64_t tiles, int64_t K, int BK) {
@@ -2234,6 +2357,23 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
 }
 
 }  // namespace
+
+int skinny_blocks(int64_t K) { return (int)std::min<int64_t>(64, std::max<int64_t>(1, (K + 2047) / 2048)); }
+
+int skinny_strided_launch(int dtype, const SkinnyArgs& a, hipStream_t stream) {
+  if (a.K <= 0 || a.nkb < 0 || a.nkb > kSkMaxKBits || (int64_t(1) << a.nkb) != a.K ||
+      (skinny_blocks(a.K) > 1 && a.W == nullptr)) {
+    set_error("skinny: bad K / workspace");
+    return TQ_ERR_INVALID;
+  }
+  switch (dtype) {
+    case TQ_F32: return skinny_strided_typed<float, false>(a, stream);
+    case TQ_C64: return skinny_strided_typed<float, true>(a, stream);
+    case TQ_F64: return skinny_strided_typed<double, false>(a, stream);
+    case TQ_C128: return skinny_strided_typed<double, true>(a, stream);
+    default: set_error("skinny: dtype"); return TQ_ERR_INVALID;
+  }
+}
 
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch) {
   int64_t bm, bn, bk;

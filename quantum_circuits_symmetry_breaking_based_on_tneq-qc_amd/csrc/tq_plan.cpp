@@ -247,7 +247,7 @@ class Compiler {
         for (auto& op : P_.ops) {
           const bool okab = (op.a.kind == BUF_ARENA || op.a.kind == BUF_PINNED) &&
                             (op.b.kind == BUF_ARENA || op.b.kind == BUF_PINNED);
-          if (op.kind != OP_GEMM || op.invariant || op.batch != 1 || op.writes_output || !okab ||
+          if (op.kind != OP_GEMM || op.skinny || op.invariant || op.batch != 1 || op.writes_output || !okab ||
               op.c.kind != BUF_ARENA || (P_.lane_stride / P_.esz) % 2)
             continue;
           op.lane_batch = true;
@@ -1741,6 +1741,92 @@ class Compiler {
     return TQ_OK;
   }
 
+  // A GEMM step whose output is tiny (M * N <= 16, no batch modes, no single-side sums) and whose
+  // operands would need a permute: one strided skinny op reads both in place (bit weights from the
+  // operands' own strides; every M / N / K mode a power of two).  true: emitted (*rc its status)
+  static bool skinny_strided_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_SKINNY_STRIDED");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
+  bool skinny_step(int s, const Live* A, const Live* B, const std::set<int>& sA, const std::set<int>& sB,
+                   const std::vector<int>& bord, const std::vector<int>& mord, const std::vector<int>& nord,
+                   const std::vector<int>& kord, bool final, Live& res, int* rc) {
+    if (!skinny_strided_enabled() || !bord.empty() || !sA.empty() || !sB.empty()) return false;
+    const int64_t M = ext_of(mord), N = ext_of(nord), K = ext_of(kord);
+    auto p2 = [](int64_t v) { return v >= 1 && (v & (v - 1)) == 0; };
+    if (!p2(M) || !p2(N) || M * N > 16 || !p2(K) || K < 256 || K > (int64_t(1) << kSkMaxKBits)) return false;
+    for (const auto* ord : {&mord, &nord, &kord})
+      for (int m : *ord) if (!p2(ext_[m])) return false;
+    if (A->buf.kind == BUF_PENDING || B->buf.kind == BUF_PENDING) return false;
+    // bit weights, least significant bit first (row-major index: the last mode is fastest)
+    auto weights = [&](const Live& X, const std::vector<int>& ord, int64_t* w, int cap) {
+      int nb = 0;
+      for (auto it = ord.rbegin(); it != ord.rend(); ++it) {
+        const int pos = X.pos(*it);
+        int e = 0;
+        while ((int64_t(1) << e) < ext_[*it]) ++e;
+        for (int b = 0; b < e; ++b) {
+          if (nb >= cap) return -1;
+          w[nb++] = X.stride[pos] << b;
+        }
+      }
+      return nb;
+    };
+    SkinnyArgs sk;
+    sk.K = K;
+    sk.M = (int)M;
+    sk.N = (int)N;
+    if (weights(*A, mord, sk.wam, 4) < 0 || weights(*B, nord, sk.wbn, 4) < 0) return false;
+    const int nka = weights(*A, kord, sk.wak, kSkMaxKBits), nkb = weights(*B, kord, sk.wbk, kSkMaxKBits);
+    if (nka < 0 || nkb < 0 || nka != nkb) return false;
+    sk.nkb = nka;
+    std::vector<int> rord = mord;
+    rord.insert(rord.end(), nord.begin(), nord.end());
+    bool direct;
+    int64_t roff;
+    BufRef tgt = result_target(final, rord, M * N, &direct, &roff);
+    Op op;
+    op.kind = OP_GEMM;
+    op.skinny = true;
+    op.sk = sk;
+    op.a = A->buf; op.b = B->buf; op.c = tgt;
+    op.writes_output = direct;
+    op.M = M; op.N = N; op.K = K; op.batch = 1;
+    const int P = skinny_blocks(K);
+    op.ws_bytes = P > 1 ? (size_t)P * M * N * P_.esz : 0;
+    op.na = A->numel();
+    op.nb = B->numel();
+    op.nc = M * N;
+    op.nws = (int64_t)((op.ws_bytes + P_.esz - 1) / P_.esz);
+    int64_t wsoff = -1;
+    if (op.ws_bytes) {
+      wsoff = arenas_[region()].alloc((int64_t)op.ws_bytes);
+      op.ws = BufRef{BUF_ARENA, 0, wsoff / (int64_t)P_.esz, region()};
+    }
+    op.step = s;
+    op.flops = (double)M * N * K * (cplx_ ? 8.0 : 2.0);
+    op.bytes = (double)(M * K + K * N + M * N) * P_.esz;
+    std::ostringstream o;
+    o << "step " << s << " SKINNY M=" << M << " N=" << N << " K=" << K << " (strided, no permutes)"
+      << (direct ? " ->OUT" : "");
+    op.note = o.str();
+    P_.ops.push_back(op);
+    if (wsoff >= 0) arenas_[region()].release(wsoff);
+    res.modes = rord;
+    res.ext.clear();
+    for (int m : rord) res.ext.push_back(ext_[m]);
+    res.stride = contig_strides(res.ext);
+    res.buf = tgt;
+    res.owned = !direct;
+    *rc = TQ_OK;
+    if (final && !direct)
+      *rc = emit_permute(res, P_.out_modes, {}, BufRef{BUF_OUTPUT, 0, 0}, true, s, "result->out");
+    return true;
+  }
+
   struct GemmChoice {
     bool swap = false;          // roles: A = second operand
     int korder_from = 0;        // 0: A's order, 1: B's order
@@ -1801,6 +1887,10 @@ class Compiler {
     Cand c = *best;
     const int64_t bsz = ext_of(c.bord), M = ext_of(c.mord), N = ext_of(c.nord),
                   K = ext_of(c.kord);
+    if (!(c.a_ok && c.b_ok)) {
+      int rc = 0;
+      if (skinny_step(s, c.A, c.B, c.sA, c.sB, c.bord, c.mord, c.nord, c.kord, final, res, &rc)) return rc;
+    }
     // materialise operands
     BufRef abuf = c.A->buf, bbuf = c.B->buf;
     int64_t aoff = -1, boff = -1;
@@ -2179,6 +2269,16 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
                                   ptr(op.a), ptr(op.c), beta, st));
           break;
         case OP_GEMM: {
+          if (op.skinny) {
+            SkinnyArgs a = op.sk;
+            a.A = ptr(op.a);
+            a.B = ptr(op.b);
+            a.C = ptr(op.c);
+            a.W = op.ws_bytes ? ptr(op.ws) : nullptr;
+            a.beta = beta;
+            TQ_TRY(skinny_strided_launch(P.dtype, a, st));
+            break;
+          }
           GemmPresplit ps;
           const bool pre = P.run_mode && op.ps_cand;
           if (pre) {

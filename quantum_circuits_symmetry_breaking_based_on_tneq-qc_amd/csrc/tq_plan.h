@@ -81,6 +81,10 @@ struct Op {
   // lane_sum (a lane-batched GEMM): its result is read only by one output permute, so the
   // lanes' results are summed into lane 0's and that permute (lane_once) runs once per batch
   bool lane_sum = false, lane_once = false;
+  // strided skinny contraction (an OP_GEMM with M * N <= 16 whose operands are read in place
+  // through per-bit strides instead of being permuted first): weights in sk, pointers at launch
+  bool skinny = false;
+  SkinnyArgs sk;
   // element counts of a / b / c / ws (hazard analysis of the launch schedule)
   int64_t na = 0, nb = 0, nc = 0, nws = 0;
   // bookkeeping

@@ -13,6 +13,7 @@ contracted symbols from the inputs and sums the sub-contractions.
 from __future__ import annotations
 
 import ctypes
+import math
 import operator
 import threading
 import weakref
@@ -279,6 +280,31 @@ class HipContractExpression:
         return out
 
 
+def _in_place_order(mi, mj, res, ext):
+    """Mode order of a pairwise result written in place into the larger operand's layout: its
+    kept modes where they are, the smaller operand's new modes at the first contracted one."""
+    size = lambda ms: math.prod(ext[m] for m in ms)
+    big, small = (mi, mj) if size(mi) >= size(mj) else (mj, mi)
+    keep = set(res)
+    new = [m for m in small if m in keep and m not in big]
+    out, put = [], False
+    for m in big:
+        if m in keep:
+            out.append(m)
+        elif not put:
+            out.extend(new)
+            put = True
+    if not put:
+        out.extend(new)
+    return tuple(out) if set(out) == keep and len(out) == len(keep) else None
+
+
+def _writes_through_permute(e: "HipContractExpression") -> bool:
+    """True when the step's plan ends with a permute of its result into the requested order."""
+    p = NativePlan(e.net, e.path, torch.complex64, None, [])
+    return "result->out" in p.describe()
+
+
 class _ReverseTree:
     """Reverse-mode differentiation through the expression's pairwise path.
 
@@ -310,25 +336,60 @@ class _ReverseTree:
         last = len(expr.path) - 1
         s2 = lambda ms: "".join(sym[m] for m in ms)
         shp = lambda ms: tuple(ext[m] for m in ms)
+        fsteps = []
         for s, (i, j) in enumerate(expr.path):
             res = st.result(i, j)
             if s == last:
                 res = tuple(net.out)      # the final step writes the output's mode order
             k = st.contract(i, j)
             mi, mj = self.modes[i], self.modes[j]
-            self.modes[k] = res
-            fwd = HipContractExpression(f"{s2(mi)},{s2(mj)}->{s2(res)}", shp(mi), shp(mj), optimize=[(0, 1)])
+            fwd = None
+            if s != last:
+                # an intermediate's mode order is free: prefer the one the step's kernel writes in
+                # place (a small operand absorbed into a large one: its new modes where the
+                # contracted ones were), which saves the step's output permute
+                nat = _in_place_order(mi, mj, res, ext)
+                if nat is not None and nat != tuple(res):
+                    cand = HipContractExpression(f"{s2(mi)},{s2(mj)}->{s2(nat)}", shp(mi), shp(mj),
+                                                 optimize=[(0, 1)])
+                    if not _writes_through_permute(cand):
+                        fwd, res = cand, nat
+            self.modes[k] = tuple(res)
+            if fwd is None:
+                fwd = HipContractExpression(f"{s2(mi)},{s2(mj)}->{s2(res)}", shp(mi), shp(mj), optimize=[(0, 1)])
+            fsteps.append((i, j, k, fwd))
+        # gradient (conjugated) of every node: the inputs' in their own order, an intermediate's in
+        # the order its gradient step writes in place (chosen in reverse, consumers first)
+        self.hmodes: Dict[int, Tuple[int, ...]] = {i: self.modes[i] for i in range(self.n_in)}
+        if fsteps:
+            self.hmodes[fsteps[-1][2]] = self.modes[fsteps[-1][2]]
+        bwds = {}
+        for (i, j, k, fwd) in reversed(fsteps):
+            hk = self.hmodes[k]
             bwd = []
-            for a, other, m_a, m_o in ((i, j, mi, mj), (j, i, mj, mi)):
-                avail = set(res) | set(m_o)
+            for a, other in ((i, j), (j, i)):
+                m_a, m_o = self.modes[a], self.modes[other]
+                avail = set(hk) | set(m_o)
                 extra = [m for m in m_a if m not in avail]          # broadcast back via ones
-                terms = [s2(res), s2(m_o)] + [sym[m] for m in extra]
-                shapes = [shp(res), shp(m_o)] + [(ext[m],) for m in extra]
+                terms = [s2(hk), s2(m_o)] + [sym[m] for m in extra]
+                shapes = [shp(hk), shp(m_o)] + [(ext[m],) for m in extra]
                 nt = 2 + len(extra)          # SSA path: (0, 1), then each ones vector joins
                 path = [(0, 1)] + [(1 + t, nt + t - 1) for t in range(1, 1 + len(extra))]
-                g = HipContractExpression(",".join(terms) + "->" + s2(m_a), *shapes, optimize=path)
+                g = None
+                h_a = m_a
+                if a >= self.n_in and not extra:
+                    nat = _in_place_order(hk, m_o, m_a, ext)
+                    if nat is not None and nat != tuple(m_a):
+                        cand = HipContractExpression(",".join(terms) + "->" + s2(nat), *shapes, optimize=path)
+                        if not _writes_through_permute(cand):
+                            g, h_a = cand, nat
+                if g is None:
+                    g = HipContractExpression(",".join(terms) + "->" + s2(m_a), *shapes, optimize=path)
+                self.hmodes[a] = tuple(h_a)
                 bwd.append((a, other, g, [ext[m] for m in extra]))
-            self.steps.append((i, j, k, fwd, bwd))
+            bwds[k] = bwd
+        for (i, j, k, fwd) in fsteps:
+            self.steps.append((i, j, k, fwd, bwds[k]))
         self.final = self.n_in + len(expr.path) - 1 if expr.path else 0
         self.single = None
         if not expr.path:   # one operand: a transpose / single-side sum of it
@@ -352,6 +413,7 @@ class _TreeRuntime:
         self.stream = torch.cuda.current_stream(device).cuda_stream   # the stream it is keyed on
         t = tree
         shape = lambda n: tuple(t.ext[m] for m in t.modes[n])
+        hshape = lambda n: tuple(t.ext[m] for m in t.hmodes[n])
         with torch.cuda.device(device):
             self.vals = {k: torch.empty(shape(k), dtype=dtype, device=device) for (_, _, k, _, _) in t.steps}
             # conjugated gradients: the inputs' in one flat buffer (one conj at the end), the
@@ -364,7 +426,7 @@ class _TreeRuntime:
                 self.h[i] = self.flat[off:off + n].view(shape(i))
                 off += n
             for (_, _, k, _, _) in t.steps:
-                self.h[k] = torch.empty(shape(k), dtype=dtype, device=device)
+                self.h[k] = torch.empty(hshape(k), dtype=dtype, device=device)
             self.ones = {}
             for (_, _, _, _, bwd) in t.steps:
                 for (_, _, _, exts) in bwd:

@@ -301,3 +301,32 @@ def test_gemm_skinny(T, dev, dt, M, N, K, B, beta):
         ref = np.matmul(aa.astype(hi), bb.astype(hi)) + beta * c0.astype(hi)
         err = np.abs(cd.cpu().numpy() - ref).max() / np.abs(ref).max()
         assert err < TOL[dt], (ta, tb, err)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("nm,nn,nk", [(2, 2, 12), (3, 1, 10), (0, 4, 9), (1, 0, 14), (4, 0, 8)])
+def test_skinny_strided_step(T, dev, dt, nm, nn, nk):
+    """A pairwise step with a tiny result (2^(nm+nn) <= 16 elements) whose operands would need
+    permutes: the plan reads both in place through per-bit strides (SKINNY op), modes in shuffled
+    orders on both sides, against numpy's einsum in the exact dtype."""
+    from tneq_qc_amd.einsum import get_symbol
+    from tneq_qc_amd.expression import HipContractExpression
+    rng = np.random.default_rng(nm * 100 + nn * 10 + nk)
+    kk = list(range(nk))
+    mm = list(range(nk, nk + nm))
+    nnm = list(range(nk + nm, nk + nm + nn))
+    a_modes = list(rng.permutation(kk + mm))
+    b_modes = list(rng.permutation(kk + nnm))
+    out = list(rng.permutation(mm + nnm)) if (nm + nn) else []
+    sym = lambda ms: "".join(get_symbol(int(m)) for m in ms)
+    eq = f"{sym(a_modes)},{sym(b_modes)}->{sym(out)}"
+    a = _rand(rng, (2,) * len(a_modes), dt)
+    b = _rand(rng, (2,) * len(b_modes), dt)
+    e = HipContractExpression(eq, a.shape, b.shape, optimize=[(0, 1)])
+    desc = e.plan(T.from_numpy(a).dtype).describe()
+    assert "SKINNY" in desc, desc
+    got = e(_to(T, dev, a), _to(T, dev, b)).cpu().numpy()
+    hi = "complex128" if dt.startswith("complex") else "float64"
+    ref = np.einsum(eq, a.astype(hi), b.astype(hi))
+    err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30)
+    assert err < TOL[dt], (eq, err)
