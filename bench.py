@@ -259,8 +259,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group backend for N > 1 (nccl = RCCL over xGMI)")
     ap.add_argument("--save-out", default=None, help="rank 0 saves the last step's amplitudes (.npy)")
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 training-step line")
