@@ -354,7 +354,7 @@ def main():
     g3m = bool(L.tq_library_query(b"gemm_3m") == 1)
     bf16 = bool(L.tq_library_query(b"gemm_bf16") == 1)
     f16 = bf16 and bool(L.tq_library_query(b"gemm_f16") == 1)
-    f16_g3 = f16 and L.tq_library_query(b"gemm_f16_var") in (2, 5, 6, 7, 8)   # Gauss 3M on the f16 terms
+    f16_g3 = f16 and L.tq_library_query(b"gemm_f16_var") in (2, 5, 6, 7, 8, 9)   # Gauss 3M on the f16 terms
     value = n_amp * args.steps / dt
     nl = max(1, gemm["launches"])
     avg_gemm_s = gemm["ms"] / 1e3 / nl

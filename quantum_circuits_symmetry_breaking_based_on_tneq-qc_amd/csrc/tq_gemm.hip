@@ -82,7 +82,7 @@ bool gemm_configure(const char* key, int64_t v) {
   if (k == "gemm_bf16") { g_gemm_bf16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16") { g_gemm_f16 = v ? 1 : 0; return true; }
   if (k == "gemm_f16_var") {
-    if (v < 0 || v > 8) return false;
+    if (v < 0 || v > 9) return false;
     g_gemm_f16_var = (int)v;
     return true;
   }
@@ -659,8 +659,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 template <int WMW_, int WNW_, int TI_, int TJ_, int NTERM_, int NSET_, bool ILV_, bool G3_ = false,
-          int SLOTS_ = 2, bool ORD_ = false, bool POUT_ = false, bool STG_ = false>
+          int SLOTS_ = 2, bool ORD_ = false, bool POUT_ = false, bool STG_ = false, bool PIPE_ = false>
 struct Tile {
+  // PIPE (with STG): the step's barrier sits before its last product group, whose MFMAs then run
+  // under the reads of the NEXT step's first group: a step starts on fragments already in
+  // registers instead of waiting for its first LDS reads
+  static constexpr bool PIPE = PIPE_;
   // STG (with POUT): a K-step's fragments are read one product group (re / im / re+im planes) at
   // a time, group h+1's under group h's MFMAs: two groups' fragments live instead of three
   static constexpr bool STG = STG_;
@@ -711,6 +715,8 @@ using TileH8G3 = Tile<2, 4, 2, 1, 2, 3, true, true, 2, true>;
 using TileH8GP = Tile<2, 4, 2, 1, 2, 2, true, true, 2, false, true>;
 // product-major order, fragments read per product group, 3 staging sets (var 8)
 using TileH8GS = Tile<2, 4, 2, 1, 2, 3, true, true, 2, false, true, true>;
+// var 8 with the barrier before the last product group, next step's first group read early (var 9)
+using TileH8GQ = Tile<2, 4, 2, 1, 2, 3, true, true, 2, false, true, true, true>;
 // f16, one barrier per two K-steps (TQ_GEMM_F16_VAR=3): the default tile on a 4-slot LDS ring
 using TileH2 = Tile<2, 4, 2, 1, 2, 4, true, false, 4>;
 
@@ -1164,6 +1170,33 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
     constexpr int P = decltype(par)::value;
     load(std::integral_constant<int, P % NSET>{}, t + NSET < nkt ? t + NSET : nkt - 1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (TL::PIPE) {
+      static_assert(TL::STG, "pipelined groups: staged group reads");
+      // group 0 of this step is in registers (read behind the previous step's barrier)
+      const char* sb = lds + (P & 1) * BUF;
+      read_group(sb, 1, fa, fb);
+      store_stage(std::integral_constant<int, (P + 1) % NSET>{}, (P & 1) ^ 1);
+      mfma_group(0, fa, fb);
+      read_group(sb, 2, fa, fb);
+      mfma_group(1, fa, fb);
+      constexpr int NMG = SP::NPAIR * TI * TJ;
+      constexpr int NRG = NTM * (TI + TJ);
+      constexpr int NWR = 2 * NGRP * NTM;
+      constexpr int E = 2 * NMG / NWR > 0 ? 2 * NMG / NWR : 1;
+      __builtin_amdgcn_sched_group_barrier(0x100, NRG, 0);
+      Interleave<0, NMG, 6, E>::run();
+      __builtin_amdgcn_sched_group_barrier(0x100, NRG, 0);
+      Interleave<NMG, 2 * NMG, 6, E>::run();
+      __builtin_amdgcn_sched_barrier(0);
+      // the split of step t + 1 is in LDS, this step's reads of its buffer are done
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      read_group(lds + ((P & 1) ^ 1) * BUF, 0, fa, fb);   // step t + 1, group 0
+      mfma_group(2, fa, fb);
+      __builtin_amdgcn_sched_group_barrier(0x100, NRG, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMG, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     if constexpr (TL::STG) {
       static_assert(TL::POUT && TL::ILV, "staged group reads: product-major, interleaved");
       const char* sb = lds + (P & 1) * BUF;
@@ -1269,6 +1302,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   if constexpr (NSET >= 4) load(std::integral_constant<int, NSET >= 4 ? 3 : 0>{}, nkt > 3 ? 3 : nkt - 1);
   store_stage(std::integral_constant<int, 0>{}, 0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if constexpr (TL::PIPE) read_group(lds, 0, fa, fb);
   int t = 0;
   for (; t + U < nkt; t += U) {
     body(I0{}, t);
@@ -1286,8 +1320,17 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
     if (t + 4 < nkt) body(I3{}, t + 3);
     if (t + 5 < nkt) body(I4{}, t + 4);
   }
-  read_frags(lds + ((nkt - 1) & 1) * BUF, fa, fb);
-  mfmas(fa, fb);  // step nkt - 1
+  if constexpr (TL::PIPE) {   // step nkt - 1: group 0 already in registers
+    const char* sb = lds + ((nkt - 1) & 1) * BUF;
+    read_group(sb, 1, fa, fb);
+    read_group(sb, 2, fa, fb);
+    mfma_group(0, fa, fb);
+    mfma_group(1, fa, fb);
+    mfma_group(2, fa, fb);
+  } else {
+    read_frags(lds + ((nkt - 1) & 1) * BUF, fa, fb);
+    mfmas(fa, fb);  // step nkt - 1
+  }
   }
 
   const bool partial = g.splits > 1;
@@ -2197,7 +2240,10 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
             f.bad = ps->bad;
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH, xbf::SplitPre>), dim3((unsigned)nb),
                                dim3(xbf::TileH::NT), 0, stream, f);
-          } else if (var == 8)
+          } else if (var == 9)
+            hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8GQ, xbf::SplitF16>), dim3((unsigned)nb),
+                               dim3(xbf::TileH8GQ::NT), 0, stream, f);
+          else if (var == 8)
             hipLaunchKernelGGL((gemm_c64_kouter_split_kernel<xbf::TileH8GS, xbf::SplitF16>), dim3((unsigned)nb),
                                dim3(xbf::TileH8GS::NT), 0, stream, f);
           else if (var == 7)

@@ -133,7 +133,7 @@ def test_contract_pair_gate_apply(T, dev):
     assert np.abs(c - ref).max() / np.abs(ref).max() < 1e-5
 
 
-@pytest.fixture(params=["f16", "f16w4", "f16g3", "f16r4", "f16s16", "f16g3w8", "f16g3o", "f16g3p", "f16g3s", "bf16", "f32"])
+@pytest.fixture(params=["f16", "f16w4", "f16g3", "f16r4", "f16s16", "f16g3w8", "f16g3o", "f16g3p", "f16g3s", "f16g3q", "bf16", "f32"])
 def c64_kernel(request):
     """Runs a test once on each complex64 K-outer kernel: the f16 2-term split of the scaled
     operands (default tile; "f16w4": 4 waves of 64x64, "f16g3": the same with Gauss's 3M
@@ -142,8 +142,9 @@ def c64_kernel(request):
     fall back to the default kernel), "f16g3w8": the 64 x 32 tile with Gauss's 3M product, "f16g3o":
     the same with 3 staging sets and the ordered term pairs (the library default), "f16g3p":
     "f16g3w8" with product-major MFMA order, "f16g3s": product-major with the fragments read per
-    product group and 3 staging sets — tq_library_set("gemm_f16_var", 1 / 2 / 3 / 4 / 5 / 6 / 7 /
-    8)), the bf16
+    product group and 3 staging sets, "f16g3q": "f16g3s" with the barrier before the last group
+    and the next step's first group read under it — tq_library_set("gemm_f16_var", 1 / 2 / 3 / 4 /
+    5 / 6 / 7 / 8 / 9)), the bf16
     3-term split kernel
     (tq_library_set("gemm_f16", 0)) and the f32-MFMA LDS-DMA kernel (tq_library_set("gemm_bf16",
     0)); restores the defaults."""
@@ -154,7 +155,7 @@ def c64_kernel(request):
     p = request.param
     assert L.tq_library_set(b"gemm_bf16", 0 if p == "f32" else 1) == 0
     assert L.tq_library_set(b"gemm_f16", 1 if p.startswith("f16") else 0) == 0
-    assert L.tq_library_set(b"gemm_f16_var", {"f16w4": 1, "f16g3": 2, "f16r4": 3, "f16s16": 4, "f16g3w8": 5, "f16g3o": 6, "f16g3p": 7, "f16g3s": 8}.get(p, 0)) == 0
+    assert L.tq_library_set(b"gemm_f16_var", {"f16w4": 1, "f16g3": 2, "f16r4": 3, "f16s16": 4, "f16g3w8": 5, "f16g3o": 6, "f16g3p": 7, "f16g3s": 8, "f16g3q": 9}.get(p, 0)) == 0
     yield p
     for k, v in zip(keys, before):
         L.tq_library_set(k, v)
