@@ -223,12 +223,25 @@ def alt_gemm(args, var: str, desc: str):
     import subprocess
     env = dict(os.environ, **{var: "0"})
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", args.config, "--steps", str(args.steps),
-           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt"]
+           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
     return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
             "gemm": f"{desc} ({var}=0)", "roofline": d["roofline"]}
+
+
+def other_config(args, cfg: str):
+    """BASELINE.json's other amplitude configs (C2: 30q depth-14, one amplitude, no slicing;
+    C3: 40q depth-16, 64 slices) timed the same way on the same box, in a child process (each
+    builds its own plan and arena); the headline stays C4."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    return {k: d[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "hbm_kernels") if k in d}
 
 
 def launch_ranks(args, argv) -> int:
@@ -266,6 +279,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 training-step line")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the f32-MFMA GEMM headline (TQ_GEMM_BF16=0, a child process)")
+    ap.add_argument("--no-other", action="store_true",
+                    help="skip the C2 / C3 secondary lines (child processes, N=1 only)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args, sys.argv[1:]))
@@ -497,6 +512,13 @@ def main():
                 res[key] = alt_gemm(args, var, desc)
             except Exception as e:  # the alternate lines must never hide the headline
                 res[key] = {"error": repr(e)}
+    if world == 1 and rank == 0 and args.config == "C4" and not args.no_other:
+        for cfg in ("C2", "C3"):
+            _log(f"secondary config {cfg}")
+            try:
+                res[f"config_{cfg}"] = other_config(args, cfg)
+            except Exception as e:  # the secondary lines must never hide the headline
+                res[f"config_{cfg}"] = {"error": repr(e)}
     if not args.no_c5:   # every rank runs its share of the candidates
         if rank == 0:
             _log("C5 training line")

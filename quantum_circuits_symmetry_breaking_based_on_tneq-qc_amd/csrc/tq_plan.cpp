@@ -924,9 +924,10 @@ class Compiler {
     }();
     return v;
   }
-  // slices per batch when the per-slice working set is small (TQ_SLICE_LANES, default 8; 1 = off)
+  // slices per batch when the per-slice working set is small (TQ_SLICE_LANES, default 16; 1 = off;
+  // C3 with the capped sweep2 launches: 1.27 ms per step at 8 lanes, 1.18 at 16)
   // arena the lane copies may add in total (TQ_LANE_ARENA_MB, default 6 GiB of the 288 GB):
-  // C3's 6-MiB per-slice part gets 8 lanes, C4's 1.1 GiB gets 4 (measured: 16.4 -> 15.9 ms/step)
+  // C3's 6-MiB per-slice part gets 16 lanes, C4's 1.1 GiB gets 4 (measured: 16.4 -> 15.9 ms/step)
   static size_t lane_arena_budget() {
     static const size_t v = [] {
       const char* e = getenv("TQ_LANE_ARENA_MB");
@@ -937,7 +938,7 @@ class Compiler {
   static int slice_lanes() {
     static const int v = [] {
       const char* e = getenv("TQ_SLICE_LANES");
-      return e ? std::max(1, std::min(16, atoi(e))) : 8;
+      return e ? std::max(1, std::min(16, atoi(e))) : 16;
     }();
     return v;
   }

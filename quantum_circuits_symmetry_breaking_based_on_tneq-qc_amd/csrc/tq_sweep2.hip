@@ -752,20 +752,24 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
   int blocks = 0;
   for (int q = 0; q < L.nops; ++q) blocks = std::max(blocks, L.op[q].block_begin + L.op[q].nblocks);
   if (blocks <= 0) return TQ_OK;
-  // Opt-in (TQ_S2_CAP=1): a launch of more workgroups than fit on the GPU at once (the
-  // lane-merged per-slice levels: 8 ops x 512 chunks) scaled to one resident round, every
-  // workgroup striding over more chunks -- to amortize the ~5-us workgroup prologue.  Measured on
-  // C4: 295 vs 276 us for the 4096-workgroup level (the extra rounds overlap their prologues with
-  // the previous round's chunks), so it stays off.
+  // A launch of more workgroups than fit on the GPU at once (the lane-merged per-slice levels:
+  // 8-16 lanes x 2 ops x 64-512 chunks) is scaled to one resident round (TQ_S2_CAP = rounds,
+  // default 1; 0 = off): every workgroup strides over several chunks, so its ~5-us prologue
+  // (descriptor + tables) is paid once and each chunk's stores drain under the next chunk's gate
+  // passes (the chunk pipeline below) instead of at the end of a one-chunk workgroup.  Measured
+  // (r03, same box): C3 1.84 -> 1.27 ms per step (its per-slice launch of 1536 one-chunk
+  // workgroups spent ~80 us per round in the store / drain phases, waves waiting 75 %), C4 +-0
+  // (13.36 / 13.29 ms; 2 rounds 13.29, 4 rounds 13.24), C3 with 2 rounds 1.56 ms.
   static const int cap = [] {
     const char* e = getenv("TQ_S2_CAP");
-    if (!e || e[0] != '1') return 0;
+    const double rounds = e ? atof(e) : 1.0;   // resident rounds per launch (0 = no cap)
+    if (!(rounds > 0)) return 0;
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&sweep2_kernel<T, CB>), NT, 0) != hipSuccess)
       return 0;
-    return cus * std::max(1, per);
+    return std::max(1, (int)(cus * std::max(1, per) * rounds));
   }();
   if (cap > 0 && blocks > cap) {
     S2Launch R = L;

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-B="python3 bench.py --no-cpu-baseline --no-c5 --no-alt"
+B="python3 bench.py --no-cpu-baseline --no-c5 --no-alt --no-other"
 for v in "$@"; do
   echo "== bench var $v"
   TQ_GEMM_F16_VAR=$v timeout -k 10 200 $B --steps 20 > gpurun_out/ab_b$v.log 2>&1 || exit 1

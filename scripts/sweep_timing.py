@@ -2,7 +2,8 @@
 """Phase timing of every sweep2 op of one C4 execute (development aid).  Needs libtneqhip.so
 built with -DTQ_S2_TIMING (make EXTRA=-DTQ_S2_TIMING): workgroup 0 of each op stamps the wall
 clock (100 MHz) at: start, descriptor staged, tables built, first chunk in LDS, first chunk's
-gates done, first chunk stored, end.  Prints per-op phase durations in us."""
+gates done, first chunk stored, end.  Prints per-op phase durations in us.
+    TNEQHIP_LIB=<timing build> python scripts/sweep_timing.py [C4|C3|C2] [slices]"""
 import ctypes, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -22,11 +23,12 @@ expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=t
 dev = torch.device("cuda:0")
 ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
 out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
+SR = (0, int(sys.argv[2]) if len(sys.argv) > 2 else 1, 1)   # slices of the timed execute
 for _ in range(3):
-    expr(*ops, out=out, slice_range=(0, 1, 1))
+    expr(*ops, out=out, slice_range=SR)
 torch.cuda.synchronize()
 f(buf, NREC)  # drain
-expr(*ops, out=out, slice_range=(0, 1, 1))
+expr(*ops, out=out, slice_range=SR)
 torch.cuda.synchronize()
 n = f(buf, NREC)
 a = np.frombuffer(buf, dtype=np.uint64, count=n * W).reshape(n, W).astype(np.int64)

@@ -13,7 +13,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-COMMON = ["--config", "C4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-c5", "--no-alt"]
+COMMON = ["--config", "C4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
 
 
 def _run(args, out):
