@@ -949,6 +949,16 @@ class Compiler {
     }();
     return v;
   }
+  // narrowest chunk (log2 columns) of a sweep2 op before the tile / min-chunk caps (TQ_S2_LC):
+  // 7 since r03 (C3's per-slice ops, 128-element tiles: 32 -> 128 columns per chunk, 1.16 ->
+  // 1.04 ms per step with the capped launches; C4 and C2 +-0; 8-10 no better)
+  static int s2_base_logc() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_LC");
+      return e ? std::max(0, std::min(10, atoi(e))) : 7;
+    }();
+    return v;
+  }
   static bool s2_blocks_enabled() {
     static const int v = [] {
       const char* e = getenv("TQ_S2_BLOCKS");
@@ -1171,7 +1181,7 @@ class Compiler {
     for (size_t j = 0; j < cb.size(); ++j) { d.w_in[j] = cb[j].first; d.w_out[j] = cb[j].second; }
     const int lc_cap = s2_chunk_bits((int)P_.esz) - used;
     if (lc_cap < 0) return false;
-    int lc = std::max(5, d.colbits - 10);
+    int lc = std::max(s2_base_logc(), d.colbits - 10);
     lc = std::min(lc, lc_cap);
     lc = std::min(lc, d.colbits);
     // small tensors: narrower chunks, so that the op still spreads over >= s2_min_chunks()
