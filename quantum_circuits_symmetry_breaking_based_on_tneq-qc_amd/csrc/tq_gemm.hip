@@ -768,6 +768,21 @@ struct SplitF16 {
   // the packed f16 halves directly), v_cvt_pk_f16_f32 (l): 3 VALU per value
   template <int N>
   static __device__ __forceinline__ void split(const float (&v)[N], int sc, uint32_t (&t)[2][N / 2]) {
+#ifdef TQ_GEMM_DIAG_HALFSPLIT
+    // development diagnostic (wrong results): h as in the split, l = h with flipped low bits (4
+    // VALU per pair instead of 6) -- the split's VALU cost at the same data flow.  Measured r03:
+    // 5.17 -> 5.08 ms per C4 launch (-1.7 %), clock +1 %: all of the split's VALU is worth ~5 %
+    // (raw f32 bits as the terms instead, no VALU, ran 9.7 ms: NaN / Inf f16 patterns)
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) {
+      const float x0 = ldexpf(v[2 * j], sc), x1 = ldexpf(v[2 * j + 1], sc);
+      const f16x2 hv = {(_Float16)x0, (_Float16)x1};
+      const uint32_t h = __builtin_bit_cast(uint32_t, hv);
+      t[0][j] = h;
+      t[1][j] = h ^ 0x00030003u;
+    }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < N / 2; ++j) {
       const float x0 = ldexpf(v[2 * j], sc), x1 = ldexpf(v[2 * j + 1], sc);
