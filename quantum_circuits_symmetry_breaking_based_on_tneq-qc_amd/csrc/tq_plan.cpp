@@ -1160,6 +1160,7 @@ class Compiler {
       for (int t = 0; t < G.K * G.N; ++t) {
         G.gidx[t] = g.d.gtab.empty() ? t : g.d.gtab[t];
         if (G.gidx[t] >= kS2GateRaw) return false;   // the kernel stages kS2GateRaw elements per gate
+        d.cgidx[j][t] = (uint8_t)G.gidx[t];
       }
     }
     // the final working set must be the output tile
@@ -1178,7 +1179,7 @@ class Compiler {
     if ((int)cb.size() > kS2MaxColBits) return false;
     d.colbits = (int)cb.size();
     d.ncols = int64_t(1) << d.colbits;
-    for (size_t j = 0; j < cb.size(); ++j) { d.w_in[j] = cb[j].first; d.w_out[j] = cb[j].second; }
+    for (size_t j = 0; j < cb.size(); ++j) { d.k.w_in[j] = cb[j].first; d.k.w_out[j] = cb[j].second; }
     const int lc_cap = s2_chunk_bits((int)P_.esz) - used;
     if (lc_cap < 0) return false;
     int lc = std::max(s2_base_logc(), d.colbits - 10);
@@ -1331,11 +1332,11 @@ class Compiler {
     for (int r = 0; r < kS2MaxSlots; ++r) {
       const int ri = r % rin, ro = r % rout;
       for (int b = kS2LogThreads; b < d.nld; ++b)
-        if ((ri >> (b - kS2LogThreads)) & 1) { d.ld_hm[r] += d.ld_w[b]; d.ld_hc[r] ^= d.ld_code[b]; }
+        if ((ri >> (b - kS2LogThreads)) & 1) { d.k.ld_hm[r] += d.ld_w[b]; d.ld_hc[r] ^= d.ld_code[b]; }
       for (int b = kS2LogThreads; b < d.nst; ++b)
-        if ((ro >> (b - kS2LogThreads)) & 1) { d.st_hm[r] += d.st_w[b]; d.st_hc[r] ^= d.st_code[b]; }
-      d.ld_ha[r] = lds_addr(d.ld_hc[r]);
-      d.st_ha[r] = lds_addr(d.st_hc[r]);
+        if ((ro >> (b - kS2LogThreads)) & 1) { d.k.st_hm[r] += d.st_w[b]; d.st_hc[r] ^= d.st_code[b]; }
+      d.k.ld_ha[r] = lds_addr(d.ld_hc[r]);
+      d.k.st_ha[r] = lds_addr(d.st_hc[r]);
     }
     auto swz = [&](int bits) {
       int v = 0;
@@ -1359,7 +1360,7 @@ class Compiler {
     // gate fields and group tables (what the kernel used to build per workgroup)
     for (size_t j = 0; j < c.gates.size(); ++j) {
       const S2Gate& G = d.gate[j];
-      int32_t* gm = d.gmeta[j];
+      int32_t* gm = d.k.gmeta[j];
       gm[kS2GmK] = G.K;
       gm[kS2GmN] = G.N;
       gm[kS2GmPass] = (int32_t)G.pass_mask;
@@ -1375,7 +1376,7 @@ class Compiler {
           if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
           if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
         }
-        d.lut[j][jj] = (base << d.logC) ^ (sw & cmask);
+        d.k.lut[j][jj] = ((base << d.logC) ^ (sw & cmask)) * (int32_t)P_.esz;   // bytes
       }
     }
     // passes: register blocks of consecutive square gates (S2Desc::pmeta), single gates otherwise
@@ -1392,13 +1393,13 @@ class Compiler {
             if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
             if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
           }
-          lut[jj] = (base << d.logC) ^ (sw & cmask);
+          lut[jj] = ((base << d.logC) ^ (sw & cmask)) * (int32_t)P_.esz;   // bytes
         }
       };
       int j = 0;
       d.npass = 0;
       while (j < ng) {
-        int32_t* pm = d.pmeta[d.npass++];
+        int32_t* pm = d.k.pmeta[d.npass++];
         pm[kS2PmFirst] = j;
         uint32_t bm = 0, live = 0;
         const int e = block_span(j, ng, &bm, &live);
@@ -1428,7 +1429,7 @@ class Compiler {
           if (G.K == 4) code |= (local(__builtin_ctz((uint32_t)kdep[q][2])) << 2) | 16;
           pm[kS2PmCode + (q - j)] = code;
         }
-        group_lut(live & ~bm, d.lut[j]);
+        group_lut(live & ~bm, d.k.lut[j]);
         j = e;
       }
     }

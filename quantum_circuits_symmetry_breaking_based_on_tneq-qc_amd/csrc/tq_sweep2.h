@@ -5,6 +5,7 @@
 // LDS tile index; a gate reads its K inputs and writes its N outputs at the positions of its
 // index bits (outputs reuse the positions the gate frees), so the tile is updated in place.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 #include <hip/hip_runtime.h>
@@ -39,31 +40,19 @@ struct S2Gate {
   int32_t gidx[kS2MaxKN * kS2MaxKN] = {};             // coefficient k*N+n -> element of G
 };
 
-struct S2Desc {
-  int64_t ncols = 0, nchunks = 0;
-  int logC = 0, colbits = 0;     // columns per chunk (log2), column index bits
-  int nld = 0, nst = 0;          // chunk bits of the load (X) / store (Y) enumerations
-  int ngates = 0;
-  // 1 + index of the last gate when the store phase applies it in registers (0: every gate is a
-  // pass): its output index bits are the lowest register-slot bits of the store enumeration, so
-  // a thread's slots r0 .. r0+N-1 hold one group's outputs and r0 .. r0+K-1 its inputs
-  int epi = 0;
-  int64_t ld_w[16] = {}, st_w[16] = {};      // memory weight of each chunk bit (ascending)
-  int32_t ld_code[16] = {}, st_code[16] = {};
-  // LDS element address of each chunk bit: every LDS address is an XOR of these
-  int32_t ld_a[16] = {}, st_a[16] = {};
+// The tables every chunk and gate pass of the kernel reads: staged from the descriptor straight
+// into their own LDS block once per workgroup and kept for the whole launch.
+struct S2Keep {
   // register slot r (chunk bits >= kS2LogThreads of element r*512+tid): memory offset and LDS
   // address; slots beyond the chunk repeat slot r % slots (a duplicate, harmless access)
   int64_t ld_hm[kS2MaxSlots] = {}, st_hm[kS2MaxSlots] = {};
-  int32_t ld_ha[kS2MaxSlots] = {}, st_ha[kS2MaxSlots] = {};
-  int32_t ld_hc[kS2MaxSlots] = {}, st_hc[kS2MaxSlots] = {};
   int64_t w_in[kS2MaxColBits] = {}, w_out[kS2MaxColBits] = {};  // column-bit weights
-  int32_t vsw[12] = {};          // swizzle vector of each position (kS2MaxPos used)
-  S2Gate gate[kS2MaxGates];
-  // Built on the host (plan compile) and copied to LDS verbatim by the kernel:
-  //  lut[g][j]: LDS address part of group index bits -> (pass positions << logC) ^ swizzle, j < 32
-  //             for the low 5 pass bits, 32 + j for the high ones (XOR-linear, combined by ^)
-  //  gmeta[g][f]: K, N, pass mask, kaddr[0..3], naddr[0..7] (kS2GmK.. layout)
+  int32_t ld_ha[kS2MaxSlots] = {}, st_ha[kS2MaxSlots] = {};
+  // Built on the host (plan compile):
+  //  lut[g][j]: LDS BYTE offset part of group index bits -> ((pass positions << logC) ^ swizzle)
+  //             * element size, j < 32 for the low 5 pass bits, 32 + j for the high ones
+  //             (XOR-linear, combined by ^)
+  //  gmeta[g][f]: K, N, pass mask, kaddr[0..3], naddr[0..7] (kS2GmK.. layout; element units)
   int32_t lut[kS2MaxGates][64] = {};
   int32_t gmeta[kS2MaxGates][16] = {};
   // Passes over the tile (one barrier each).  A pass is one gate, or a register block: a run of
@@ -74,9 +63,36 @@ struct S2Desc {
   //            block), block-bit address parts [4, 4+B), per-gate local codes [8, 8+count):
   //            bits 0-1 / 2-3 = block bits of the gate's index bits 0 / 1, bit 4 = 4x4 (else 2x2)
   //  a block's group table replaces lut[first gate]
-  int32_t npass = 0, pad2 = 0;
   int32_t pmeta[kS2MaxGates][16] = {};
 };
+
+struct S2Desc {
+  // ---- staged into the (not yet used) tile buffer, read in the kernel's prologue only
+  int64_t ncols = 0, nchunks = 0;
+  int logC = 0, colbits = 0;     // columns per chunk (log2), column index bits
+  int nld = 0, nst = 0;          // chunk bits of the load (X) / store (Y) enumerations
+  int ngates = 0;
+  // 1 + index of the last gate when the store phase applies it in registers (0: every gate is a
+  // pass): its output index bits are the lowest register-slot bits of the store enumeration, so
+  // a thread's slots r0 .. r0+N-1 hold one group's outputs and r0 .. r0+K-1 its inputs
+  int epi = 0;
+  int64_t ld_w[16] = {}, st_w[16] = {};      // memory weight of each chunk bit (ascending)
+  // LDS element address of each chunk bit: every LDS address is an XOR of these
+  int32_t ld_a[16] = {}, st_a[16] = {};
+  // coefficient k*N+n of gate g -> element of its gate tensor (S2Gate::gidx, < kS2GateRaw)
+  uint8_t cgidx[kS2MaxGates][kS2MaxK * kS2MaxKN] = {};
+  int32_t npass = 0, pad2 = 0;
+  // ---- kept in LDS for the whole launch
+  S2Keep k;
+  // ---- host-side build records (not staged)
+  int32_t ld_code[16] = {}, st_code[16] = {};
+  int32_t ld_hc[kS2MaxSlots] = {}, st_hc[kS2MaxSlots] = {};
+  int32_t vsw[12] = {};          // swizzle vector of each position (kS2MaxPos used)
+  alignas(8) S2Gate gate[kS2MaxGates];
+};
+constexpr int kS2KeepOff = (int)offsetof(S2Desc, k);
+constexpr int kS2DescHotBytes = (int)(offsetof(S2Desc, k) + sizeof(S2Keep));   // the staged part
+static_assert(kS2KeepOff % 8 == 0 && kS2DescHotBytes % 8 == 0, "descriptor copy granularity");
 constexpr int kS2GmK = 0, kS2GmN = 1, kS2GmPass = 2, kS2GmKaddr = 3, kS2GmNaddr = kS2GmKaddr + kS2MaxK;
 static_assert(kS2GmNaddr + kS2MaxKN <= 16, "gate meta layout");
 constexpr int kS2PmFirst = 0, kS2PmCount = 1, kS2PmB = 2, kS2PmPass = 3, kS2PmAddr = 4, kS2PmCode = 8;

@@ -46,15 +46,9 @@ constexpr int kCf = kS2MaxK * kS2MaxKN;      // coefficient slots per gate
 constexpr int kGmK = kS2GmK, kGmN = kS2GmN, kGmPass = kS2GmPass, kGmKaddr = kS2GmKaddr,
               kGmNaddr = kS2GmNaddr;
 constexpr int kGm = 16;
-constexpr int kDescWords2 = (int)(sizeof(S2Desc) / 8);
-static_assert(sizeof(S2Desc) % 8 == 0, "descriptor copy granularity");
+constexpr int kDescWords2 = kS2DescHotBytes / 8;   // the kernel-read part of S2Desc
+constexpr int kKeepWords2 = kS2KeepOff / 8;        // words before S2Desc::k (-> tile buffer)
 
-// per-chunk tables of the load / store phases, staged in LDS for the same reason
-struct S2Hot {
-  int64_t ld_hm[kS2MaxSlots], st_hm[kS2MaxSlots];
-  int64_t w_in[kS2MaxColBits], w_out[kS2MaxColBits];
-  int32_t ld_ha[kS2MaxSlots], st_ha[kS2MaxSlots];
-};
 static_assert(kGmNaddr + kS2MaxKN <= kGm, "gate meta layout");
 static_assert(kLut == 64, "lut layout shared with S2Desc::lut");
 
@@ -385,11 +379,13 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   static_assert(sizeof(Raw) == sizeof(T), "raw slot word");
   static_assert(RMAX <= kS2MaxSlots, "register slots");
   __shared__ T buf[1 << CB];
-  __shared__ int32_t lut[kS2MaxGates * kLut];            // group -> LDS address part
   __shared__ T cf[kS2MaxGates * kCf];                    // gate coefficients, k*N+n
-  __shared__ int32_t gmeta[kS2MaxGates * kGm];           // K, N, pass mask, kaddr, naddr
-  __shared__ int32_t pmeta[kS2MaxGates * 16];            // passes (S2Desc::pmeta)
-  __shared__ S2Hot hot;
+  static_assert(sizeof(S2Keep) % 8 == 0, "kept-table copy granularity");
+  __shared__ uint2 keep_raw[sizeof(S2Keep) / 8];          // S2Desc::k, staged once
+  const S2Keep& keep = *reinterpret_cast<const S2Keep*>(keep_raw);
+  const int32_t* const gmeta = &keep.gmeta[0][0];        // K, N, pass mask, kaddr, naddr
+  const int32_t* const pmeta = &keep.pmeta[0][0];        // passes
+  const int32_t* const lut = &keep.lut[0][0];            // group -> LDS byte offset part
   const int tid = threadIdx.x;
   // ---- which op this workgroup works on (wave-uniform scan over <= 16 ranges)
   int j = 0;
@@ -407,16 +403,18 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   if (ts_rec && threadIdx.x == 0)
     for (int q = 9; q < kTsPh; ++q) g_s2_ts[ts_idx][q] = 0;
 #endif
-  // ---- the descriptor is staged in the (not yet used) tile buffer by one coalesced pass; the
-  // tables below are built from that copy (no chains of dependent scalar loads)
-  // the gate tensors' raw elements go to the tile buffer behind the descriptor in the same pass
-  // (pointers and element counts are kernel arguments)
-  constexpr int kGrawOff = ((int)sizeof(S2Desc) + 255) / 256 * 256 / (int)sizeof(T);
+  // ---- the descriptor is staged by one coalesced pass: its prologue part into the (not yet
+  // used) tile buffer, S2Desc::k straight into its own LDS block, kept for the whole launch (no
+  // chains of dependent scalar loads, no second LDS copy); the gate tensors' raw elements go to
+  // the tile buffer behind the prologue part in the same pass (pointers and element counts are
+  // kernel arguments)
+  constexpr int kGrawOff = (kS2KeepOff + 255) / 256 * 256 / (int)sizeof(T);
   static_assert(kGrawOff + kS2MaxGates * kS2GateRaw <= (1 << CB), "descriptor + raw gates fit the tile");
   T* graw = buf + kGrawOff;
   {
     const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(d);
     uint2* bd = reinterpret_cast<uint2*>(buf);
+    uint2* kd = keep_raw;
     // every load is issued before the first LDS store (one memory round trip, not one per
     // loop iteration)
     constexpr int kIt = (kDescWords2 + NT - 1) / NT, kGt = (kS2MaxGates * kS2GateRaw + NT - 1) / NT;
@@ -436,7 +434,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
       const int i = tid + it * NT;
-      if (i < kDescWords2) bd[i] = dw[it];
+      if (i < kKeepWords2) bd[i] = dw[it];
+      else if (i < kDescWords2) kd[i - kKeepWords2] = dw[it];
     }
 #pragma unroll
     for (int it = 0; it < kGt; ++it) {
@@ -517,7 +516,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       for (int q = 0; q < 8; ++q) {
         const int b = b0 + q;
         const int bb = b < kS2MaxColBits ? b : kS2MaxColBits - 1;
-        const int64_t wi = ds->w_in[bb], wo = ds->w_out[bb];
+        const int64_t wi = keep.w_in[bb], wo = keep.w_out[bb];
         const bool on = b >= logC && b < colbits && ((chl >> (b - logC)) & 1);
         cb_in += on ? wi : 0;
         cb_out += on ? wo : 0;
@@ -529,8 +528,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), i);
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
   };
-  auto base_in = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_in, i) : chunk_base(ch, hot.w_in); };
-  auto base_out = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_out, i) : chunk_base(ch, hot.w_out); };
+  auto base_in = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_in, i) : chunk_base(ch, keep.w_in); };
+  auto base_out = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_out, i) : chunk_base(ch, keep.w_out); };
   // The first chunk is loaded into RMAX register slots before the tables are staged (those
   // registers are free again before the gate passes).  Inside the chunk loop only chunks of at
   // most RPF slots are prefetched under the gate passes (the register-block passes need the
@@ -557,51 +556,33 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   auto prefetch = [&](int i, int64_t ch) {
     if (!pf) return;
     const int64_t base = base_in(i, ch);
-    TQ_BY_COUNT(RPF, rin, reg[r] = *lane_at(Xr + uniform(base + hot.ld_hm[r]), ldo));
+    TQ_BY_COUNT(RPF, rin, reg[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
   };
   auto fill = [&](int i, int64_t ch) {   // the chunk's elements -> tile
     if (pf) {
-      TQ_BY_COUNT(RPF, rin, bufr[lda ^ hot.ld_ha[r]] = reg[r]);
+      TQ_BY_COUNT(RPF, rin, bufr[lda ^ keep.ld_ha[r]] = reg[r]);
       return;
     }
     const int64_t base = base_in(i, ch);
     Raw t[RMAX];
-    TQ_BY_COUNT(RMAX, rin, t[r] = *lane_at(Xr + uniform(base + hot.ld_hm[r]), ldo));
-    TQ_BY_COUNT(RMAX, rin, bufr[lda ^ hot.ld_ha[r]] = t[r]);
+    TQ_BY_COUNT(RMAX, rin, t[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
+    TQ_BY_COUNT(RMAX, rin, bufr[lda ^ keep.ld_ha[r]] = t[r]);
   };
   Raw reg0[RMAX];
   // ---- the first chunk's loads go out now (addresses from the staged descriptor) and land
   // while the tables are staged
   int64_t ch = lb;
   if (ch < nchunks) {
-    const int64_t base = lane_bases ? lane64(cb_in, 0) : chunk_base(ch, ds->w_in);
-    TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + ds->ld_hm[r]), ldo));
+    const int64_t base = lane_bases ? lane64(cb_in, 0) : chunk_base(ch, keep.w_in);
+    TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
   }
   TQ_TS(41);   // first chunk's loads issued
   // ---- gate coefficients -> LDS
   for (int i = tid; i < ngates * kCf; i += NT) {
     const int g = i / kCf, t = i % kCf;
-    const S2Gate& gt = ds->gate[g];
-    if (t < gt.K * gt.N) cf[i] = graw[g * kS2GateRaw + gt.gidx[t]];
+    if (t < keep.gmeta[g][kS2GmK] * keep.gmeta[g][kS2GmN]) cf[i] = graw[g * kS2GateRaw + ds->cgidx[g][t]];
   }
   TQ_TS(42);   // coefficients staged
-  // ---- per-chunk tables -> LDS
-  for (int i = tid; i < kS2MaxSlots; i += NT) {
-    hot.ld_hm[i] = ds->ld_hm[i];
-    hot.st_hm[i] = ds->st_hm[i];
-    hot.ld_ha[i] = ds->ld_ha[i];
-    hot.st_ha[i] = ds->st_ha[i];
-  }
-  for (int i = tid; i < kS2MaxColBits; i += NT) {
-    hot.w_in[i] = ds->w_in[i];
-    hot.w_out[i] = ds->w_out[i];
-  }
-  // ---- gate fields and group tables -> LDS (built on the host, S2Desc::gmeta / lut; the
-  // LUT entries become byte offsets)
-  for (int i = tid; i < ngates * kGm; i += NT) gmeta[i] = ds->gmeta[i / kGm][i % kGm];
-  for (int i = tid; i < npass * 16; i += NT) pmeta[i] = ds->pmeta[i / 16][i % 16];
-  constexpr int kSh = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;
-  for (int i = tid; i < ngates * kLut; i += NT) lut[i] = ds->lut[i / kLut][i % kLut] << kSh;
   TQ_TS(43);   // tables staged (before the barrier)
   __syncthreads();   // every wave is done with the descriptor copy: the tile may be written
   TQ_TS(2);
@@ -611,7 +592,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   //   next chunk's loads -> gate passes -> wait(all) -> store this chunk -> tile <- next chunk
   // the stores of a chunk then drain under the next chunk's gate passes and the loads of the
   // chunk after it, instead of being waited for before that chunk can enter the tile.
-  if (ch < nchunks) TQ_BY_COUNT(RMAX, rin, bufr[lda ^ hot.ld_ha[r]] = reg0[r]);
+  if (ch < nchunks) TQ_BY_COUNT(RMAX, rin, bufr[lda ^ keep.ld_ha[r]] = reg0[r]);
   __syncthreads();
   TQ_TS(3);
 #ifdef TQ_S2_TIMING
@@ -656,11 +637,11 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
         for (int r0 = 0; r0 < rout; r0 += 4) {
           T t[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ hot.st_ha[r0 + q]];
+          for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ keep.st_ha[r0 + q]];
           if (st_lane) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + q]), sto);
+              T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + q]), sto);
               const T v = use_beta ? scale_add(t[q], *p, beta) : t[q];
               TQ_ST(p, stored(v));
               if constexpr (TRK) track(v);
@@ -670,10 +651,10 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
         }
       } else {
         T t[4];
-        TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ hot.st_ha[r]]);
+        TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ keep.st_ha[r]]);
         if (st_lane) {
           TQ_BY_COUNT(4, rout, {
-            T* p = lane_at(Y + uniform(base + hot.st_hm[r]), sto);
+            T* p = lane_at(Y + uniform(base + keep.st_hm[r]), sto);
             const T v = use_beta ? scale_add(t[r], *p, beta) : t[r];
             TQ_ST(p, stored(v));
             if constexpr (TRK) track(v);
@@ -694,14 +675,14 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       for (int r0 = 0; r0 < rout; r0 += N) {
         T x[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) x[k] = buf[sta ^ hot.st_ha[r0 + k]];
+        for (int k = 0; k < K; ++k) x[k] = buf[sta ^ keep.st_ha[r0 + k]];
         if (st_lane) {
 #pragma unroll
           for (int n = 0; n < N; ++n) {
             T acc = mul(x[0], c[n]);
 #pragma unroll
             for (int k = 1; k < K; ++k) mac(acc, x[k], c[k * N + n]);
-            T* p = lane_at(Y + uniform(base + hot.st_hm[r0 + n]), sto);
+            T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + n]), sto);
             const T v = use_beta ? scale_add(acc, *p, beta) : acc;
             TQ_ST(p, stored(v));
             if constexpr (TRK) track(v);
