@@ -668,7 +668,12 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     auto store_epi = [&](auto kt, auto nt, auto tracked) {
       constexpr int K = decltype(kt)::value, N = decltype(nt)::value;
       constexpr bool TRK = decltype(tracked)::value;
-      const T* ce = cf + (epi - 1) * kCf;
+      // the coefficient row's offset is re-materialised per chunk: hoisted out of the chunk loop,
+      // the per-case LDS addresses of every (K, N) instantiation were spilled to scratch and
+      // reloaded one dependent round trip per read
+      int cb = __builtin_amdgcn_readfirstlane((epi - 1) * kCf);
+      asm volatile("" : "+s"(cb));
+      const T* ce = cf + cb;
       T c[K * N];
 #pragma unroll
       for (int q = 0; q < K * N; ++q) c[q] = uniform(ce[q]);
