@@ -2421,15 +2421,26 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
         for (int j = 0; j < (lanes_merge ? (int)lane_sl.size() : 1); ++j)
           for (int q : grp) (P.ops[q].s2_dense ? dense : items).push_back({lanes_merge ? j : cur, q});
         const int keep = cur;
-        // dense ops (tq_sweepd.hip): their own launches, one input tile size each
+        // dense ops (tq_sweepd.hip): their own launches, at most two input tile sizes each
+        // (TQ_S2D_MIX=0: one)
+        static const bool s2d_mix = [] {
+          const char* e = getenv("TQ_S2D_MIX");
+          return !(e && e[0] == '0');
+        }();
+        static const bool s2d_nt = [] {
+          const char* e = getenv("TQ_S2D_NT");
+          return e && e[0] == '1';
+        }();
         while (!dense.empty()) {
           S2DLaunch L;
           const int tin = P.ops[dense[0].second].tin;
+          int tin2 = 0;
           std::vector<std::pair<int, int>> rest;
           int blocks = 0;
           for (auto& it : dense) {
             const Op& op = P.ops[it.second];
-            if (op.tin != tin || L.nops == kS2MaxOps) { rest.push_back(it); continue; }
+            if (op.tin != tin && tin2 == 0 && s2d_mix && !s2d_nt) tin2 = op.tin;
+            if ((op.tin != tin && op.tin != tin2) || L.nops == kS2MaxOps) { rest.push_back(it); continue; }
             set_lane(it.first);
             S2DOp& o = L.op[L.nops++];
             o.desc = (const S2Dense*)((const char*)P.d_tables + P.stab_off[op.stab]);

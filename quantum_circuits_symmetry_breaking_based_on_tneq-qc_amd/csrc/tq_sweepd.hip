@@ -31,6 +31,7 @@
 // tout x tin coefficients (32 KiB at tin 16) stream through the scalar cache once per column
 // group.  Algorithmic bytes per op = (numel(X) + numel(Y)) * 8; 8 * tin flops per output.
 #include <type_traits>
+#include <utility>
 
 #include "tq_common.h"
 #include "tq_sweep2.h"
@@ -67,18 +68,25 @@ constexpr int kLevels = 7;            // column-base tables: 6 column bits each,
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int TIN, bool NTS>
-__global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
-  static_assert(TIN % 2 == 0 && TIN <= kS2DMaxTin, "k-steps of 2");
+// LDS of one workgroup: the coefficient planes Mr, Mi as [k][r] (room for TMAX input elements),
+// output offsets (elements), column-group bases (in, out) per 6-bit level, column-bit weights
+template <int TMAX>
+struct SdSmem {
+  float mp[2][TMAX * kS2DMaxTout];
+  int32_t ooff[kS2DMaxTout];
+  int64_t btab[2][kLevels][64];
+  int64_t wcol[2][kS2MaxColBits];
+};
+
+// one op's share of the launch (its workgroups stride over its 32-column tiles)
+template <int TIN, bool NTS, int TMAX>
+__device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
+  static_assert(TIN % 2 == 0 && TIN <= TMAX && TMAX <= kS2DMaxTin, "k-steps of 2");
   constexpr int KS = TIN / 2;
-  __shared__ float mp[2][TIN * kS2DMaxTout];     // planes Mr, Mi as [k][r]
-  __shared__ int32_t ooff[kS2DMaxTout];          // output offsets (elements)
-  __shared__ int64_t btab[2][kLevels][64];       // column-group bases (in, out) per 6-bit level
-  __shared__ int64_t wcol[2][kS2MaxColBits];
-  int j = 0;
-  for (int q = 1; q < L.nops; ++q)
-    if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
-  const S2DOp& op = L.op[j];
+  auto& mp = sm.mp;
+  auto& ooff = sm.ooff;
+  auto& btab = sm.btab;
+  auto& wcol = sm.wcol;
   cst<S2Dense>* d = as_const<S2Dense>(op.desc);
   const int tout = d->tout, colbits = d->colbits;
   const int tid = threadIdx.x;
@@ -191,6 +199,24 @@ __global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
   }
 }
 
+// TB == 0: every op of the launch has input tile TA; else each op has TA or TB (one dependency
+// level's dense ops of both subtrees of a cut network in one launch: their tails overlap)
+template <int TA, int TB, bool NTS>
+__global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
+  constexpr int TMAX = TA > TB ? TA : TB;
+  __shared__ SdSmem<TMAX> sm;
+  int j = 0;
+  for (int q = 1; q < L.nops; ++q)
+    if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
+  const S2DOp& op = L.op[j];
+  if constexpr (TB == 0) {
+    sweepd_op<TA, NTS, TMAX>(op, sm);
+  } else {
+    if (op.tin == TA) sweepd_op<TA, NTS, TMAX>(op, sm);
+    else sweepd_op<TB, NTS, TMAX>(op, sm);
+  }
+}
+
 }  // namespace
 
 int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
@@ -202,11 +228,16 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     set_error("sweepd: bad op count");
     return TQ_ERR_INVALID;
   }
-  const int tin = L.op[0].tin;
+  // at most two input tile sizes per launch (ta > tb; tb = 0: one)
+  int ta = L.op[0].tin, tb = 0;
   for (int q = 0; q < L.nops; ++q) {
-    if (L.op[q].tin != tin) {
-      set_error("sweepd: one input tile size per launch");
-      return TQ_ERR_INVALID;
+    const int t = L.op[q].tin;
+    if (t != ta && t != tb) {
+      if (tb != 0) {
+        set_error("sweepd: at most two input tile sizes per launch");
+        return TQ_ERR_INVALID;
+      }
+      tb = t;
     }
     // the kernel stores whole 32-output tiles and stages at most kS2DMaxTout offsets
     if (L.op[q].tout < 32 || L.op[q].tout % 32 || L.op[q].tout > kS2DMaxTout || !L.op[q].desc || !L.op[q].M) {
@@ -220,26 +251,43 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     const char* e = getenv("TQ_S2D_NT");
     return e && e[0] == '1';
   }();
+  if (tb > ta) std::swap(ta, tb);
+  auto pow2tin = [](int t) { return t == 2 || t == 4 || t == 8 || t == 16; };
+  if (!pow2tin(ta) || (tb && !pow2tin(tb))) {
+    set_error("sweepd: tin must be 2, 4, 8 or 16");
+    return TQ_ERR_INVALID;
+  }
+  if (tb && nts) {
+    set_error("sweepd: mixed input tile sizes only with plain stores");
+    return TQ_ERR_INVALID;
+  }
   const void* fn = nullptr;
-#define TQ_SD_FN(T) (nts ? reinterpret_cast<const void*>(&sweepd_kernel<T, true>) \
-                         : reinterpret_cast<const void*>(&sweepd_kernel<T, false>))
-  switch (tin) {
-    case 2: fn = TQ_SD_FN(2); break;
-    case 4: fn = TQ_SD_FN(4); break;
-    case 8: fn = TQ_SD_FN(8); break;
-    case 16: fn = TQ_SD_FN(16); break;
-    default:
-      set_error("sweepd: tin must be 2, 4, 8 or 16");
-      return TQ_ERR_INVALID;
+#define TQ_SD_FN(T) (nts ? reinterpret_cast<const void*>(&sweepd_kernel<T, 0, true>) \
+                         : reinterpret_cast<const void*>(&sweepd_kernel<T, 0, false>))
+#define TQ_SD_MIX(A, B) reinterpret_cast<const void*>(&sweepd_kernel<A, B, false>)
+  switch (ta * 32 + tb) {
+    case 2 * 32: fn = TQ_SD_FN(2); break;
+    case 4 * 32: fn = TQ_SD_FN(4); break;
+    case 8 * 32: fn = TQ_SD_FN(8); break;
+    case 16 * 32: fn = TQ_SD_FN(16); break;
+    case 4 * 32 + 2: fn = TQ_SD_MIX(4, 2); break;
+    case 8 * 32 + 2: fn = TQ_SD_MIX(8, 2); break;
+    case 8 * 32 + 4: fn = TQ_SD_MIX(8, 4); break;
+    case 16 * 32 + 2: fn = TQ_SD_MIX(16, 2); break;
+    case 16 * 32 + 4: fn = TQ_SD_MIX(16, 4); break;
+    case 16 * 32 + 8: fn = TQ_SD_MIX(16, 8); break;
+    default: break;
   }
 #undef TQ_SD_FN
-  static int slots[kS2DMaxTin + 1] = {};
-  if (!slots[tin]) {
+#undef TQ_SD_MIX
+  static int slots[(kS2DMaxTin + 1) * 32] = {};
+  const int key = ta * 32 + tb;
+  if (!slots[key]) {
     int dev = 0, cus = 0, per = 0;
     TQ_HIP(hipGetDevice(&dev));
     TQ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     TQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kWaves, 0));
-    slots[tin] = std::max(1, cus * std::max(1, per));
+    slots[key] = std::max(1, cus * std::max(1, per));
   }
   S2DLaunch R = L;
   static const int diag = [] {
@@ -248,7 +296,7 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
   }();
   int blocks = 0;
   for (int q = 0; q < R.nops; ++q) {
-    const int want = std::max(1, slots[tin] / R.nops);
+    const int want = std::max(1, slots[key] / R.nops);
     R.op[q].nblocks = std::max(1, std::min(R.op[q].nblocks, want));
     R.op[q].block_begin = blocks;
     R.op[q].pad = diag;

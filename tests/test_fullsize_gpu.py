@@ -114,6 +114,11 @@ def _production_plan_checks(e, cfg, lanes):
     d = plan.describe()
     # the lane-batched boundary GEMM fed by its producers' max words, summed over lanes
     assert " lanes" in d and "lane-sum" in d and "amax<-" in d, d
+    if cfg == "C4":
+        # both halves' per-slice expanding chains as dense ops of one level (tin 16 and 8: one
+        # mixed sweepd launch, tq_sweepd.hip)
+        dense = [l for l in d.splitlines() if "SWEEP2 DENSE" in l]
+        assert any("tin=16" in l for l in dense) and any("tin=8" in l for l in dense), dense
 
 
 @pytest.mark.timeout(900)
