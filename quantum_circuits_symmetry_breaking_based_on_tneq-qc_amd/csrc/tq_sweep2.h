@@ -15,7 +15,13 @@ namespace tq {
 constexpr int kS2MaxGates = 16;
 constexpr int kS2MaxKN = 8;            // N <= 8 per gate (coefficient slots: 8 x 8)
 constexpr int kS2MaxK = 4;             // K <= 4 per gate (exact-shape gate passes)
-constexpr int kS2MaxOps = 16;          // independent sweep ops batched into one launch
+#ifndef TQ_S2_MAX_OPS
+#define TQ_S2_MAX_OPS 32
+#endif
+// independent sweep ops batched into one launch (a level's ops of every slice lane: C3's 16
+// lanes x 2 ops in one launch -- 0.995 -> 0.785 ms per step against 16; S2Launch is a ~7-KB
+// kernel argument)
+constexpr int kS2MaxOps = TQ_S2_MAX_OPS;
 constexpr int kS2GateRaw = 64;         // gate-tensor elements staged per gate
 constexpr int kS2ChunkBytes = 65536;   // LDS tile per workgroup
 constexpr int kS2MaxChunkBits = 13;    // log2(chunk elements) for 8-byte elements
