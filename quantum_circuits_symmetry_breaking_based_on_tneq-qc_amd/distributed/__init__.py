@@ -1,6 +1,8 @@
-from .slice_reduce import (AllReduceSum, SlicedContraction, allreduce_partials, allreduce_with_grad,
-                           shard_slices)
+from .engine import ContractStage, DistributedContractPlan, DistributedEngineSiamese, PartitionConfig
+from .slice_reduce import (AllReduceSum, SlicedContraction, align_log_scales, allreduce_partials,
+                           allreduce_with_grad, shard_slices)
 from .tree import TreeContraction, partition_terms
 
-__all__ = ["AllReduceSum", "SlicedContraction", "allreduce_partials", "allreduce_with_grad", "shard_slices",
-           "TreeContraction", "partition_terms"]
+__all__ = ["AllReduceSum", "SlicedContraction", "align_log_scales", "allreduce_partials", "allreduce_with_grad",
+           "shard_slices", "TreeContraction", "partition_terms", "DistributedEngineSiamese", "PartitionConfig",
+           "ContractStage", "DistributedContractPlan"]

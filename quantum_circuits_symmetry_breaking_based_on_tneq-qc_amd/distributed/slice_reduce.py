@@ -14,6 +14,7 @@ No P2P exchange, no handshakes, no per-stage barriers: the plan is deterministic
 """
 from __future__ import annotations
 
+import math
 from typing import Callable, Optional, Sequence, Tuple
 
 import torch
@@ -58,11 +59,70 @@ def allreduce_with_grad(t: torch.Tensor, group=None) -> torch.Tensor:
     return AllReduceSum.apply(t, group)
 
 
+class _ReplicatedInputs(torch.autograd.Function):
+    """Identity on operands that every rank holds a copy of; backward sums their gradients over
+    the group (the adjoint of replicating one logical tensor to every rank: each rank's partial
+    reads its copy, so the gradient of the copy is the sum of the ranks' contributions).  One
+    flattened all_reduce for all of them."""
+
+    @staticmethod
+    def forward(ctx, group, *tensors):
+        ctx.group = group
+        ctx.meta = [(t.shape, t.dtype) for t in tensors]
+        return tuple(t.view_as(t) for t in tensors)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        flat = torch.cat([torch.view_as_real(g).reshape(-1) if g.is_complex() else g.reshape(-1)
+                          for g in grads]) if grads else None
+        if flat is not None:
+            flat = flat.to(torch.float64) if any(g.dtype in (torch.float64, torch.complex128)
+                                                 for g in grads) else flat.to(torch.float32)
+            allreduce_partials(flat, ctx.group)
+        out, off = [None], 0
+        for (shape, dt), g in zip(ctx.meta, grads):
+            n = g.numel() * (2 if g.is_complex() else 1)
+            part = flat[off:off + n]
+            off += n
+            if g.is_complex():
+                part = torch.view_as_complex(part.to(g.real.dtype).reshape(*shape, 2))
+            else:
+                part = part.to(g.dtype).reshape(shape)
+            out.append(part)
+        return tuple(out)
+
+
+def align_log_scales(t: torch.Tensor, log_scale: float, group=None) -> Tuple[torch.Tensor, float]:
+    """TNTensor partials with per-rank log-scales: one scalar all_reduce(MAX) of the log-scales,
+    then every partial is multiplied by exp(ls_r - ls_max) so that the SUM all-reduce adds
+    like-scaled values (distributed_engine.py:1462-1491).  Returns (aligned partial, ls_max)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return t, log_scale
+    dev = t.device if dist.get_backend(group) != "gloo" else torch.device("cpu")
+    m = torch.tensor([log_scale], dtype=torch.float64, device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    top = float(m.item())
+    if top == log_scale:
+        return t, top
+    return t * (math.exp(log_scale - top) if log_scale > -math.inf else 0.0), top
+
+
 class SlicedContraction:
     """Runs a sliced HipContractExpression across the ranks of a process group.
 
-    `executor(slice_range, out)` defaults to the expression's native plan; tests inject an
-    alternative per-slice executor to exercise the sharding + reduce logic on CPU (gloo).
+    `executor(slice_range, out[, *tensors])` defaults to the expression's native plan; tests
+    inject an alternative per-slice executor to exercise the sharding + reduce logic on CPU
+    (gloo).
+
+    Gradients: when autograd is on and an operand requires grad, each rank's partial comes from
+    the expression's differentiable slice range (HipContractExpression._sliced_autograd), the
+    sum is AllReduceSum (the reference's AllReduceGrad, allreduce_grad.py:13-60: backward
+    all-reduces the incoming gradient), and the replicated operands' gradients are summed over
+    the ranks (one flattened all_reduce).  With the same loss on every rank each rank then holds
+    W x the single-process gradient, the reference's AllReduceGrad semantics.  TNTensor operands: the partial's scale is the product
+    of the operands' scales; each rank normalises its partial (max |x| -> 1, the remainder in its
+    log-scale, as TNTensor.auto_scale), the log-scales are aligned to their max and the result is
+    a TNTensor (distributed_engine.py:1437-1472).
     """
 
     def __init__(self, expr, group=None, executor: Optional[Callable] = None):
@@ -72,10 +132,51 @@ class SlicedContraction:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.executor = executor
 
-    def __call__(self, *tensors, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def __call__(self, *tensors, out: Optional[torch.Tensor] = None):
+        from ..core.tn_tensor import TNTensor
         rng = shard_slices(self.expr.n_slices, self.rank, self.world)
-        if self.executor is not None:
-            out = self.executor(rng, out)
+        tn = any(isinstance(t, TNTensor) for t in tensors)
+        log_scale, sign = 0.0, 1.0
+        if tn:
+            raw = []
+            for t in tensors:
+                if isinstance(t, TNTensor):
+                    log_scale += t.log_scale
+                    sign = -sign if t.scale < 0 else sign
+                    t = t.tensor
+                raw.append(t)
+            tensors = tuple(raw)
+        grad = (torch.is_grad_enabled() and out is None
+                and any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors))
+        if grad and self.world > 1:
+            # replicated operands: their gradients are summed over the ranks in backward
+            idx = [i for i, t in enumerate(tensors) if isinstance(t, torch.Tensor) and t.requires_grad]
+            rep = _ReplicatedInputs.apply(self.group, *[tensors[i] for i in idx])
+            tensors = list(tensors)
+            for i, t in zip(idx, rep):
+                tensors[i] = t
+            tensors = tuple(tensors)
+        if grad and len(range(*rng)) == 0:
+            # no slice on this rank: a zero partial still joins the backward's collectives
+            dt = tensors[0].dtype
+            for t in tensors[1:]:
+                dt = torch.promote_types(dt, t.dtype)
+            part = torch.zeros(self.expr.out_shape, dtype=dt, device=tensors[0].device)
+            part = part + 0 * sum(t.real.sum() if t.is_complex() else t.sum()
+                                  for t in tensors if t.requires_grad)
+        elif self.executor is not None:
+            part = self.executor(rng, out, *tensors) if tensors else self.executor(rng, out)
         else:
-            out = self.expr(*tensors, out=out, slice_range=rng)
-        return allreduce_partials(out, self.group)
+            part = self.expr(*tensors, out=out, slice_range=rng)
+        if not tn:
+            return allreduce_with_grad(part, self.group) if grad else allreduce_partials(part, self.group)
+        # normalise the partial (a constant factor: no gradient through the max)
+        mx = float(part.detach().abs().max()) if part.numel() else 0.0
+        if mx > 0:
+            part = part * (sign / mx)
+            log_scale += math.log(mx)
+        elif sign < 0:
+            part = -part
+        part, top = align_log_scales(part, log_scale, self.group)
+        total = allreduce_with_grad(part, self.group) if grad else allreduce_partials(part, self.group)
+        return TNTensor(total, scale=math.exp(top) if top < 709.0 else float("inf"), log_scale=top)

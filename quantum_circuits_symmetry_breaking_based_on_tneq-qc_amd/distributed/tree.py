@@ -7,16 +7,29 @@ Reference: DistributedEngineSiamese (tneq_qc/distributed/engine/distributed_engi
   * stages 1..ceil(log2 W) (_contract_reduce_stage :997-1069): in stage s groups of 2^s ranks
     merge the left half's tensor with the right half's over their shared bonds by a K-sharded
     partial matmul + all_reduce(SUM) inside the group (_tensor_parallel_matmul :1108-1664),
-    with P2P shard exchanges, shape / scale handshakes and barriers around every stage.
+    with P2P shard exchanges (SendRecvGrad, allreduce_grad.py:149-207), TNTensor log-scale
+    exchange + max alignment (:1437-1472), shape handshakes and barriers around every stage;
+  * the whole pipeline is differentiable (contract_distributed_with_gradient :1866-1984): the
+    exchanges and the all-reduce carry their adjoints (allreduce_grad.py:13-60, 149-207).
 
 MI355X design: the partition, every stage's equation and every shape are derived from the same
-einsum on every rank, so no handshake or barrier is needed.  A stage is three collectives on the
-group's process group (RCCL over xGMI on the node): broadcast of the left half's tensor from its
-leader, broadcast of the right half's from its leader, and one all_reduce(SUM) of the partial
-products.  The K-sharding reuses index slicing: the merge expression slices the contracted bond
-legs and rank p of the group contracts slices p, p+G, ... on the native plan (slice-invariant
-work hoisted, partial sums accumulated in place).  The result ends replicated on every rank of
-the final group, in the global output's mode order.
+einsum on every rank, so no handshake or barrier is needed.  A stage is two point-to-point
+rounds inside the group, each issued as ONE batch (dist.batch_isend_irecv: a single
+ncclGroupStart/End under RCCL, so a pair's send and receive cannot block each other): the left
+half's leader sends its block (and its log-scale) to every member, the right half's leader its
+block; then the members' K-shard partials are summed at the stage leader (log-scales aligned to
+the max, as the reference) and the total sent back.  The K-sharding reuses index slicing: the
+merge expression slices the contracted bond legs and rank p of the group contracts slices p,
+p+G, ... on the native plan.  The result ends replicated on every rank of the final group, in the
+global output's mode order.
+
+Gradients (torch autograd): `_StageExchange` and `_StageReduce` are autograd Functions whose
+backward is the exact adjoint of their forward (the block broadcast's adjoint sums the members'
+gradients at the sending leader; the reduce's adjoint sums the members' output gradients and
+returns the total to every member), the local and K-shard contractions differentiate through the
+native reverse tree (HipContractExpression, sliced ranges included).  As in the reference, the
+gradient a rank receives is that of the SUM of every rank's loss: when each rank computes the
+same loss on the replicated result, W x the single-process gradient.
 """
 from __future__ import annotations
 
@@ -26,6 +39,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..core.tn_tensor import TNTensor
 from ..einsum import parse_equation
 
 
@@ -69,7 +83,9 @@ class TreeContraction:
     """Runs einsum `eq` over `shapes` partitioned across the ranks of `group`.
 
     `executor(eq, shapes, operands, slices, slice_range)` contracts one (sub-)network and
-    defaults to the native plan (HipContractExpression); CPU tests inject the oracle."""
+    defaults to the native plan (HipContractExpression); CPU tests inject the oracle (or, for
+    gradients, a differentiable torch executor).  Operands may be TNTensors: their scales are
+    carried as log-scales through the stages and the result is a TNTensor."""
 
     def __init__(self, eq: str, shapes: Sequence[Sequence[int]], group=None,
                  partitions: Optional[Sequence[Sequence[int]]] = None,
@@ -134,6 +150,7 @@ class TreeContraction:
         # stage exchanges are point-to-point within `group` (no per-stage process groups: they
         # would have to be created by every rank of the world, and `group` may be a subgroup)
         self._exprs = {}
+        self._warm = False
 
     # -- execution -----------------------------------------------------------------------
     def _contract(self, key, eq, shapes, operands, slices=(), slice_range=None):
@@ -157,14 +174,35 @@ class TreeContraction:
         eq += "->" + "".join(sym[m] for m in self.local[p])
         return eq, [tuple(net.extents[m] for m in net.terms[t]) for t in terms]
 
-    def __call__(self, *operands) -> torch.Tensor:
-        """operands: all of the network's operands (replicated inputs; each rank reads its own)."""
+    def __call__(self, *operands):
+        """operands: all of the network's operands in equation order; a rank reads only those of
+        its own partition (the others may be None).  TNTensor operands -> TNTensor result."""
         r = self.rank
+        mine = self.parts[r]
+        ref = next(o for o in operands if o is not None)
+        ref = ref.tensor if isinstance(ref, TNTensor) else ref
+        tn = any(isinstance(o, TNTensor) for o in operands if o is not None)
+        raw, log_scale, sign = [], 0.0, 1.0
+        for t in mine:
+            o = operands[t]
+            if isinstance(o, TNTensor):
+                log_scale += o.log_scale
+                sign = -sign if o.scale < 0 else sign
+                o = o.tensor
+            raw.append(o)
+        grad = torch.is_grad_enabled() and any(getattr(o, "requires_grad", False) for o in raw)
+        if self.world > 1 and not self._warm:
+            _first_use(ref, self.group)
+            self._warm = True
         eq, shapes = self.local_equation(r)
-        if self.parts[r]:
-            cur = self._contract(("local", r), eq, shapes, [operands[t] for t in self.parts[r]])
+        if mine:
+            cur = self._contract(("local", r), eq, shapes, raw)
         else:   # more ranks than operands: an empty partition is the scalar 1
-            cur = torch.ones((), dtype=operands[0].dtype, device=operands[0].device)
+            cur = torch.ones((), dtype=ref.dtype, device=ref.device)
+            if grad:
+                cur.requires_grad_()
+        if sign < 0:
+            cur = -cur
         for row in self.stages:
             for st in row:
                 if st is None:
@@ -175,18 +213,52 @@ class TreeContraction:
                 pos = r - st.g
                 H = 2 ** (st.s - 1)
                 members = [self.granks[q] for q in range(st.g, st.g + G)]
-                left = cur if pos < H else torch.empty(st.shapes[0], dtype=cur.dtype, device=cur.device)
-                right = cur if pos >= H else torch.empty(st.shapes[1], dtype=cur.dtype, device=cur.device)
-                left, right = left.contiguous(), right.contiguous()
+                meta = _StageMeta(members, H, self.granks[r], self.group, st.shapes, cur.dtype, cur.device)
                 # the left block (leader st.g) and the right block (leader st.g + H) to every
-                # member (the reference's SendRecvGrad exchange, distributed_engine.py:1697-1766)
-                _p2p_bcast([left, right], [members[0], members[H]], members, self.granks[r], self.group)
+                # member (the reference's SendRecvGrad exchange, distributed_engine.py:1697-1766),
+                # with their log-scales
+                sides = [k for k in (0, 1) if meta.me != meta.leads[k]]
+                if grad:
+                    *recv, logs = _StageExchange.apply(cur, meta, log_scale)
+                    rec, logs = dict(zip(sides, recv)), logs.tolist()
+                else:
+                    got = _exchange(cur.detach(), meta, log_scale)
+                    rec = {k: t for k, (t, _) in got.items()}
+                    logs = [got[k][1] if k in got else log_scale for k in (0, 1)]
+                left, right, log_l, log_r = _blocks(cur, rec, logs)
                 part = self._contract(("stage", st.s, st.g), st.eq, st.shapes, [left, right],
-                                      st.slice_syms, (pos, None, G)).contiguous()
-                # sum of the members' K-shard partials (allreduce_grad.py:13-60), in member order
-                _p2p_allreduce(part, members, self.granks[r], self.group)
-                cur = part
+                                      st.slice_syms, (pos, None, G))
+                # sum of the members' K-shard partials (allreduce_grad.py:13-60), in member
+                # order, log-scales aligned to the max (distributed_engine.py:1462-1472)
+                pair = log_l + log_r
+                if grad:
+                    cur, log_scale = _StageReduce.apply(part.contiguous(), meta, pair)
+                    log_scale = float(log_scale)
+                else:
+                    cur, log_scale = _reduce(part.detach().contiguous(), meta, pair)
+        if tn:
+            return TNTensor(cur, scale=_exp(log_scale), log_scale=log_scale)
+        if log_scale != 0.0:
+            cur = cur * _exp(log_scale)
         return cur
+
+
+def _exp(x: float) -> float:
+    return math.exp(x) if x < 709.0 else float("inf")
+
+
+class _StageMeta:
+    """Static description of one stage as seen by one member."""
+    __slots__ = ("members", "me", "group", "shapes", "dtype", "device", "H")
+
+    def __init__(self, members, H, me, group, shapes, dtype, device):
+        self.members, self.H, self.me, self.group = members, H, me, group
+        self.shapes, self.dtype, self.device = shapes, dtype, device
+
+    @property
+    def leads(self):
+        """(left leader, right leader): global ranks of members[0] and members[H]."""
+        return self.members[0], self.members[self.H]
 
 
 def _view(t: torch.Tensor) -> torch.Tensor:
@@ -199,48 +271,190 @@ def _staged(t: torch.Tensor, group) -> bool:
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
-def _p2p_bcast(tensors, srcs, members, me, group):
-    """tensors[i] from global rank srcs[i] to every other member: receives posted first, then
-    sends, then one wait (no ordering deadlock)."""
-    reqs, back = [], []
-    for t, src in zip(tensors, srcs):
-        if me != src:
-            buf = torch.empty(t.shape, dtype=t.dtype) if _staged(t, group) else t
-            reqs.append(dist.irecv(_view(buf), src=src, group=group))
-            if buf is not t:
-                back.append((buf, t))
-    for t, src in zip(tensors, srcs):
-        if me == src:
-            buf = t.cpu() if _staged(t, group) else t
-            for m in members:
-                if m != src:
-                    reqs.append(dist.isend(_view(buf), dst=m, group=group))
-    for q in reqs:
-        q.wait()
-    for buf, t in back:
-        t.copy_(buf)
-
-
-def _p2p_allreduce(t: torch.Tensor, members, me, group):
-    """In-place SUM over the members: the leader adds the partials in member order and sends
-    the total back (deterministic; a stage group holds at most 2^s ranks)."""
-    if len(members) == 1:
+def _first_use(ref: torch.Tensor, group):
+    """Under RCCL the first batched point-to-point call of a group must involve all of its ranks
+    (torch.distributed.batch_isend_irecv): a tiny all-reduce on the group initialises its
+    communicator before any stage subset talks."""
+    if dist.get_backend(group) == "gloo":
         return
-    lead = members[0]
-    host = t.cpu() if _staged(t, group) else t
-    v = _view(host)
-    if me == lead:
-        bufs = [torch.empty_like(v) for _ in members[1:]]
-        reqs = [dist.irecv(b, src=m, group=group) for b, m in zip(bufs, members[1:])]
-        for q in reqs:
-            q.wait()
-        for b in bufs:
-            v += b
-        reqs = [dist.isend(v, dst=m, group=group) for m in members[1:]]
-    else:
-        dist.isend(v, dst=lead, group=group).wait()
-        reqs = [dist.irecv(v, src=lead, group=group)]
-    for q in reqs:
+    dist.all_reduce(torch.zeros(1, device=ref.device), group=group)
+
+
+def _p2p(ops, group):
+    """ops: (kind 'send'|'recv', tensor, global peer).  Issued as ONE batch and waited for."""
+    if not ops:
+        return
+    p2p = [dist.P2POp(dist.isend if k == "send" else dist.irecv, _view(t), peer, group)
+           for k, t, peer in ops]
+    for q in dist.batch_isend_irecv(p2p):
         q.wait()
-    if host is not t:
-        t.copy_(host)
+
+
+class _Wire:
+    """Device tensors as they travel: host copies under gloo, the tensors themselves under RCCL."""
+
+    def __init__(self, group):
+        self.group = group
+        self.back = []
+
+    def out(self, t):
+        return t.cpu() if _staged(t, self.group) else t
+
+    def into(self, shape, dtype, device):
+        probe = torch.empty((), dtype=dtype, device=device)
+        if _staged(probe, self.group):
+            buf = torch.empty(shape, dtype=dtype)
+            dst = torch.empty(shape, dtype=dtype, device=device)
+            self.back.append((buf, dst))
+            return buf, dst
+        buf = torch.empty(shape, dtype=dtype, device=device)
+        return buf, buf
+
+    def finish(self):
+        for buf, dst in self.back:
+            dst.copy_(buf)
+
+
+def _exchange(cur, meta: _StageMeta, log_scale: float):
+    """Forward of the block broadcast: returns {0: (left, log), 1: (right, log)} for the blocks
+    this rank receives (a leader keeps its own)."""
+    mem, me = meta.members, meta.me
+    leads = meta.leads
+    w = _Wire(meta.group)
+    ops, got = [], {}
+    for side, src in enumerate(leads):
+        if me == src:
+            payload = w.out(cur.contiguous())
+            ls = w.out(torch.tensor([log_scale], dtype=torch.float64, device=cur.device))
+            for m in mem:
+                if m != src:
+                    ops += [("send", payload, m), ("send", ls, m)]
+        else:
+            buf, dst = w.into(meta.shapes[side], meta.dtype, meta.device)
+            lbuf, ldst = w.into((1,), torch.float64, meta.device)
+            ops += [("recv", buf, src), ("recv", lbuf, src)]
+            got[side] = (dst, ldst)
+    _p2p(ops, meta.group)
+    w.finish()
+    return {side: (t, float(ls.item())) for side, (t, ls) in got.items()}
+
+
+def _blocks(cur, rec: Dict[int, torch.Tensor], logs: Sequence[float]):
+    """(left, right, log_left, log_right) on this rank: the received blocks, its own for the
+    side it leads."""
+    left = rec.get(0, cur)
+    right = rec.get(1, cur)
+    return left, right, float(logs[0]), float(logs[1])
+
+
+class _StageExchange(torch.autograd.Function):
+    """Block broadcast with its adjoint (SendRecvGrad, allreduce_grad.py:149-207): forward sends
+    a leader's block to every member of the stage; backward returns to each leader the sum of the
+    members' gradients of its block."""
+
+    @staticmethod
+    def forward(ctx, cur, meta: _StageMeta, log_scale: float):
+        got = _exchange(cur.detach(), meta, log_scale)
+        ctx.meta = meta
+        ctx.sides = sorted(got)
+        ctx.cur_meta = (tuple(cur.shape), cur.dtype, cur.device)
+        logs = torch.tensor([log_scale if meta.me == src else got[k][1]
+                             for k, src in enumerate(meta.leads)], dtype=torch.float64)
+        ctx.mark_non_differentiable(logs)
+        return (*[got[k][0] for k in ctx.sides], logs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        meta = ctx.meta
+        mem, me = meta.members, meta.me
+        shape, dtype, device = ctx.cur_meta
+        gs = dict(zip(ctx.sides, grads[:len(ctx.sides)]))
+        w = _Wire(meta.group)
+        ops, acc = [], []
+        for side, src in enumerate(meta.leads):
+            if me == src:
+                for m in mem:
+                    if m != src:
+                        buf, dst = w.into(shape, dtype, device)
+                        ops.append(("recv", buf, m))
+                        acc.append(dst)
+            else:
+                g = gs.get(side)
+                g = torch.zeros(meta.shapes[side], dtype=meta.dtype, device=meta.device) if g is None else g
+                ops.append(("send", w.out(g.contiguous()), src))
+        _p2p(ops, meta.group)
+        w.finish()
+        total = torch.zeros(shape, dtype=dtype, device=device)
+        for a in acc:       # member order: deterministic
+            total = total + a
+        return total, None, None
+
+
+def _reduce(part, meta: _StageMeta, log_scale: float):
+    """Sum of the members' partials at the leader, log-scales aligned to their max, the total
+    (and the common log-scale) sent back to every member.  Returns (total, log_scale)."""
+    mem, me = meta.members, meta.me
+    if len(mem) == 1:
+        return part, log_scale
+    lead = mem[0]
+    w = _Wire(meta.group)
+    ls_t = torch.tensor([log_scale], dtype=torch.float64, device=part.device)
+    if me == lead:
+        bufs, lbufs, ops = [], [], []
+        for m in mem[1:]:
+            buf, dst = w.into(tuple(part.shape), part.dtype, part.device)
+            lbuf, ldst = w.into((1,), torch.float64, part.device)
+            ops += [("recv", buf, m), ("recv", lbuf, m)]
+            bufs.append(dst)
+            lbufs.append(ldst)
+        _p2p(ops, meta.group)
+        w.finish()
+        scales = [log_scale] + [float(l.item()) for l in lbufs]
+        top = max(scales)
+        total = part * _exp_rel(scales[0], top)
+        for b, s in zip(bufs, scales[1:]):
+            total = total + b * _exp_rel(s, top)
+        w2 = _Wire(meta.group)
+        payload = w2.out(total.contiguous())
+        lt = w2.out(torch.tensor([top], dtype=torch.float64, device=part.device))
+        ops = []
+        for m in mem[1:]:
+            ops += [("send", payload, m), ("send", lt, m)]
+        _p2p(ops, meta.group)
+        return total, top
+    ops = [("send", w.out(part.contiguous()), lead), ("send", w.out(ls_t), lead)]
+    _p2p(ops, meta.group)
+    w2 = _Wire(meta.group)
+    buf, dst = w2.into(tuple(part.shape), part.dtype, part.device)
+    lbuf, ldst = w2.into((1,), torch.float64, part.device)
+    _p2p([("recv", buf, lead), ("recv", lbuf, lead)], meta.group)
+    w2.finish()
+    return dst, float(ldst.item())
+
+
+def _exp_rel(s: float, top: float) -> float:
+    return 1.0 if s == top else (math.exp(s - top) if s > -math.inf else 0.0)
+
+
+class _StageReduce(torch.autograd.Function):
+    """The members' K-shard partial sum with its adjoint (AllReduceGrad, allreduce_grad.py:
+    13-60): every member's partial gets exp(ls_r - ls_max) x the sum of the members' output
+    gradients."""
+
+    @staticmethod
+    def forward(ctx, part, meta: _StageMeta, log_scale: float):
+        total, top = _reduce(part, meta, log_scale)
+        ctx.meta = meta
+        ctx.factor = _exp_rel(log_scale, top)
+        if total is part:
+            total = part.clone()
+        top_t = torch.tensor(top, dtype=torch.float64)
+        ctx.mark_non_differentiable(top_t)
+        return total, top_t
+
+    @staticmethod
+    def backward(ctx, g, _g_log):
+        meta = ctx.meta
+        g = g.contiguous()
+        total, _ = _reduce(g, meta, 0.0)
+        return total * ctx.factor if ctx.factor != 1.0 else total, None, None

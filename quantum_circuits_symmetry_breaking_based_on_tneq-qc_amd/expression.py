@@ -170,10 +170,66 @@ class HipContractExpression:
     # -- execution ---------------------------------------------------------------------------
     def __call__(self, *tensors, out: Optional[torch.Tensor] = None, slice_range=None,
                  accumulate: bool = False, backend=None) -> torch.Tensor:
-        if (torch.is_grad_enabled() and out is None and slice_range is None
+        if (torch.is_grad_enabled() and out is None
                 and any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors)):
-            return _HipContractFn.apply(self, *tensors)
+            if slice_range is None or not self.sliced:
+                return _HipContractFn.apply(self, *tensors)
+            return self._sliced_autograd(tensors, slice_range)
         return self._forward(*tensors, out=out, slice_range=slice_range, accumulate=accumulate)
+
+    # -- differentiable slice ranges ---------------------------------------------------------
+    def slice_expression(self) -> "HipContractExpression":
+        """The network of ONE slice: every sliced mode removed from the terms, same SSA path."""
+        hit = self._plans.get("slice_expr")
+        if hit is None:
+            sym = self.net.symbols
+            sl = set(self.sliced)
+            terms = ["".join(sym[m] for m in t if m not in sl) for t in self.net.terms]
+            shapes = [tuple(self.net.extents[m] for m in t if m not in sl) for t in self.net.terms]
+            eq = ",".join(terms) + "->" + "".join(sym[m] for m in self.net.out)
+            hit = HipContractExpression(eq, *shapes, optimize=self.path if self.path else "greedy")
+            self._plans["slice_expr"] = hit
+        return hit
+
+    def slice_values(self, s: int) -> Dict[int, int]:
+        """Mode values of slice `s`: row-major over the sliced modes, last fastest (the
+        enumeration of tq_plan_execute)."""
+        vals, rem = {}, int(s)
+        for m in reversed(self.sliced):
+            vals[m] = rem % self.net.extents[m]
+            rem //= self.net.extents[m]
+        if rem:
+            raise ValueError("slice id out of range")
+        return vals
+
+    def _sliced_autograd(self, tensors, slice_range) -> torch.Tensor:
+        """Differentiable sum of the slices `slice_range` = (begin, end, step): each slice is the
+        one-slice expression (autograd through its reverse tree) applied to `select` views of the
+        operands, so the gradient of an operand that carries a sliced mode lands in exactly the
+        entries its slices read (the reference differentiates its K-sharded partial contraction the
+        same way, distributed_engine.py:1474-1497)."""
+        begin, end, step = slice_range
+        end = self.n_slices if end is None else end
+        sub = self.slice_expression()
+        total = None
+        for s in range(begin, end, step):
+            vals = self.slice_values(s)
+            views = []
+            for t, term in zip(tensors, self.net.terms):
+                v = t
+                for ax in reversed(range(len(term))):
+                    if term[ax] in vals:
+                        v = v.select(ax, vals[term[ax]])
+                views.append(v)
+            r = sub(*views)
+            total = r if total is None else total + r
+        if total is None:
+            dt = tensors[0].dtype
+            for t in tensors[1:]:
+                dt = torch.promote_types(dt, t.dtype)
+            dev = next((t.device for t in tensors if t.device.type == "cuda"), tensors[0].device)
+            total = torch.zeros(self.out_shape, dtype=dt, device=dev)
+        return total
 
     def reverse_tree(self) -> "_ReverseTree":
         """The per-step forward / gradient expressions used by autograd (built once)."""

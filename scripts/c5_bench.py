@@ -133,12 +133,48 @@ def _log(msg):
     print(f"[c5_bench] {msg}", file=sys.stderr, flush=True)
 
 
+def cpu_forward(expr, ts):
+    """The forward as opt_einsum's ContractExpression executes it, on torch-CPU: pairwise
+    torch.tensordot along the expression's own path (the contraction ORDER is the only thing
+    taken from the HIP expression), single-side sums, then the permute into the step's result
+    order.  Differentiable by torch autograd."""
+    from tneq_qc_amd.einsum import _State
+    st = _State(expr.net)
+    vals = dict(enumerate(ts))
+    modes = {i: tuple(t) for i, t in enumerate(expr.net.terms)}
+    for s, (i, j) in enumerate(expr.path):
+        res = st.result(i, j)
+        k = st.contract(i, j)
+        mi, mj = modes[i], modes[j]
+        ci = [q for q, m in enumerate(mi) if m in mj]
+        cj = [mj.index(mi[q]) for q in ci]
+        out = torch.tensordot(vals[i], vals[j], dims=(ci, cj))
+        om = [m for m in mi if m not in mj] + [m for m in mj if m not in mi]
+        final = tuple(expr.net.out) if s == len(expr.path) - 1 else res
+        keep = [m for m in om if m in final]
+        if len(keep) != len(om):   # single-side sums
+            out = out.sum(dim=[q for q, m in enumerate(om) if m not in final])
+        out = out.permute([keep.index(m) for m in final])
+        vals[k], modes[k] = out, final
+    return vals[max(vals)]
+
+
+def cpu_train_step(expr, ps, state, tgt, rng=random):
+    """One candidate-step on the host: cpu_forward + fidelity loss + torch autograd + the
+    reference SGDG math (oracle/optim_ref.py, the retraction draw from `rng`).  `ps` (numpy
+    arrays) are updated in place; returns (loss, gradients)."""
+    from oracle.optim_ref import sgdg_step
+    ts = [torch.tensor(p, requires_grad=True) for p in ps]
+    loss = fidelity_loss(cpu_forward(expr, ts), tgt)
+    grads = [g.numpy().copy() for g in torch.autograd.grad(loss, ts)]
+    sgdg_step(ps, [g.copy() for g in grads], state, lr=1e-2, momentum=0.9, stiefel=True, rng=rng)
+    return float(loss.detach()), grads
+
+
 def cpu_step_sample(target_np, cands, steps, budget_s=10.0):
     """torch-CPU pairwise tensordot along the same path + autograd + the reference SGDG math:
     up to `steps` steps of every candidate, stopping once `budget_s` seconds of work are done
     (at least one candidate-step)."""
-    from oracle.optim_ref import sgdg_step
-    from tneq_qc_amd.einsum import _State
     tgt = torch.from_numpy(target_np)
     items = []
     for expr, params, _, bw, _, _ in cands:
@@ -149,27 +185,7 @@ def cpu_step_sample(target_np, cands, steps, budget_s=10.0):
         for expr, ps, state in items:
             if n and time.perf_counter() - t0 > budget_s:
                 return (time.perf_counter() - t0), n
-            ts = [torch.tensor(p, requires_grad=True) for p in ps]
-            st = _State(expr.net)
-            vals = dict(enumerate(ts))
-            modes = {i: tuple(t) for i, t in enumerate(expr.net.terms)}
-            for s, (i, j) in enumerate(expr.path):
-                res = st.result(i, j)
-                k = st.contract(i, j)
-                mi, mj = modes[i], modes[j]
-                ci = [q for q, m in enumerate(mi) if m in mj]
-                cj = [mj.index(mi[q]) for q in ci]
-                out = torch.tensordot(vals[i], vals[j], dims=(ci, cj))
-                om = [m for m in mi if m not in mj] + [m for m in mj if m not in mi]
-                final = tuple(expr.net.out) if s == len(expr.path) - 1 else res
-                keep = [m for m in om if m in final]
-                if len(keep) != len(om):   # single-side sums
-                    out = out.sum(dim=[q for q, m in enumerate(om) if m not in final])
-                out = out.permute([keep.index(m) for m in final])
-                vals[k], modes[k] = out, final
-            loss = fidelity_loss(vals[max(vals)], tgt)
-            grads = torch.autograd.grad(loss, ts)
-            sgdg_step(ps, [g.numpy().copy() for g in grads], state, lr=1e-2, momentum=0.9, stiefel=True)
+            cpu_train_step(expr, ps, state, tgt)
             n += 1
     return (time.perf_counter() - t0), n
 

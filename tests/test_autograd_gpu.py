@@ -1,8 +1,10 @@
 """Reverse-mode autograd through the HIP expression's pairwise path (expression._ReverseTree)
 vs torch.einsum autograd on the CPU (complex128 / float64 reference): random networks with
 batch modes, single-side sums and broadcast-back gradients, mixed real / complex operands,
-partial requires_grad, and the symmetry-breaking fidelity loss on the masked 8-qubit ansatz
-(symmetry_breaking_quantum.py:203-224).  Tolerance 1e-10 (float64 / complex128)."""
+partial requires_grad, and the symmetry-breaking fidelity loss (symmetry_breaking_quantum.py:
+203-224) on a 5-qubit brick wall (torch.einsum, the CPU reference here, takes <= 52 symbols; the
+full 8-qubit C5 ansatz is pinned in tests/test_c5_parity_gpu.py against pairwise tensordot).
+Tolerance 1e-10 (float64 / complex128)."""
 import numpy as np
 import pytest
 

@@ -133,3 +133,132 @@ def test_partition_rule_matches_reference():
                                       list(range(27, 35))]
     assert partition_terms(3, 4) == [[0], [1], [2], []]
     assert partition_terms(6, 2, [[0, 2, 4], [1, 3, 5]]) == [[0, 2, 4], [1, 3, 5]]
+
+
+def _torch_executor(eq, shapes, operands, slices, slice_range):
+    """Differentiable stand-in for the native plan on CPU: torch.einsum per slice on `select`
+    views (the same slice enumeration as tq_plan_execute: row-major over `slices`)."""
+    lhs, rhs = eq.split("->")
+    terms = lhs.split(",")
+    if not slices:
+        return torch.einsum(eq, *operands)
+    ext = {}
+    for t, o in zip(terms, operands):
+        for c, e in zip(t, o.shape):
+            ext[c] = e
+    n = int(np.prod([ext[c] for c in slices]))
+    b, e, st = slice_range
+    e = n if e is None else e
+    sub = ",".join("".join(c for c in t if c not in slices) for t in terms) + "->" + rhs
+    acc = None
+    for sid in range(b, e, st):
+        vals, rem = {}, sid
+        for c in reversed(slices):
+            vals[c] = rem % ext[c]
+            rem //= ext[c]
+        views = []
+        for t, o in zip(terms, operands):
+            v = o
+            for ax in reversed(range(len(t))):
+                if t[ax] in vals:
+                    v = v.select(ax, vals[t[ax]])
+            views.append(v)
+        r = torch.einsum(sub, *views)
+        acc = r if acc is None else acc + r
+    if acc is None:
+        acc = torch.zeros(tuple(ext[c] for c in rhs), dtype=operands[0].dtype)
+    return acc
+
+
+def _loss(out, w):
+    return (out * w).real.sum() + (out.abs() ** 2).sum()
+
+
+def _grad_worker(rank, world, port, q):
+    """Gradients through the tree (the reference's contract_distributed_with_gradient pipeline):
+    every rank computes the same loss on the replicated result; the gradient a rank gets for its
+    own operands is that of the sum of the ranks' losses = world x the single-process gradient
+    (distributed_engine.py:1866-1984 with AllReduceGrad / SendRecvGrad adjoints)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tneq_qc_amd.distributed import TreeContraction
+        eq, shapes, ops = _network()
+        rng = np.random.default_rng(7)
+        job = TreeContraction(eq, shapes, executor=_torch_executor)
+        oshape = [job.net.extents[m] for m in job.net.out]
+        w = torch.tensor(rng.standard_normal(oshape) + 1j * rng.standard_normal(oshape))
+        ts = [torch.tensor(o, requires_grad=True) for o in ops]
+        out = job(*ts)
+        g = torch.autograd.grad(_loss(out, w), ts, allow_unused=True)
+        ref_ts = [torch.tensor(o, requires_grad=True) for o in ops]
+        ref_out = torch.einsum(eq, *ref_ts)
+        ref_g = torch.autograd.grad(_loss(ref_out, w), ref_ts)
+        err_out = float((out.detach() - ref_out.detach()).abs().max())
+        errs = []
+        for t in job.parts[rank]:
+            errs.append(float((g[t] - world * ref_g[t]).abs().max() / ref_g[t].abs().max()))
+        # operands of the other partitions are not read on this rank
+        unused = all(g[t] is None for p, terms in enumerate(job.parts) if p != rank for t in terms)
+        q.put((rank, err_out, max(errs) if errs else 0.0, unused))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_tree_contraction_gradients(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, err_out, err_g, unused in sorted(q.get(timeout=5) for _ in range(world)):
+        assert err_out < 1e-12, (rank, err_out)
+        assert err_g < 1e-10, (rank, err_g)
+        assert unused, rank
+
+
+def _scale_worker(rank, world, port, q):
+    """TNTensor operands: the scales travel as log-scales through the stages (the reference's
+    log-scale exchange + max alignment, distributed_engine.py:1437-1472); the result is a
+    TNTensor whose value equals the plain contraction."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle.contract_ref import contract
+        from tneq_qc_amd.core.tn_tensor import TNTensor
+        from tneq_qc_amd.distributed import TreeContraction
+        eq, shapes, ops = _network()
+        full = contract(eq, *ops)
+        tn = []
+        for i, o in enumerate(ops):
+            s = 2.0 ** (7 * (i % 5) - 14) * (-1 if i % 7 == 3 else 1)
+            tn.append(TNTensor(torch.from_numpy(o / s), scale=s))
+        job = TreeContraction(eq, shapes, executor=_oracle_executor)
+        res = job(*tn)
+        assert isinstance(res, TNTensor)
+        val = res.tensor.numpy() * np.exp(res.log_scale) * np.sign(res.scale)
+        q.put((rank, float(np.abs(val - full).max() / np.abs(full).max())))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tree_contraction_tntensor_scales(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scale_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, err in sorted(q.get(timeout=5) for _ in range(world)):
+        assert err < 1e-12, (rank, err)
