@@ -89,7 +89,8 @@ def _cpu_model() -> str:
 
 def _cpu_sample(t, n_sl, min_seconds, threads):
     """Whole slices of the oracle's complex64 executor at `threads` BLAS threads until
-    ~min_seconds of CPU work: (slices timed, seconds, BLAS threads in effect)."""
+    ~min_seconds of CPU work: (slices timed, seconds, BLAS threads in effect).  A network with
+    fewer slices than that takes (C2: one, unsliced) is contracted again, slice by slice."""
     import numpy as np
     from oracle.contract_ref import contract as ref_contract, sliced_operands
     from threadpoolctl import threadpool_info, threadpool_limits
@@ -97,8 +98,8 @@ def _cpu_sample(t, n_sl, min_seconds, threads):
     with threadpool_limits(limits=threads):
         used = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
         done, dt = 0, 0.0
-        while done < n_sl and dt < min_seconds:
-            eq, sops = sliced_operands(t.eq, ops64, t.sliced, done)
+        while dt < min_seconds and (done < n_sl or dt < 0.5 * min_seconds):
+            eq, sops = sliced_operands(t.eq, ops64, t.sliced, done % n_sl)
             t0 = time.perf_counter()
             ref_contract(eq, *sops, path=t.path, exact=False)
             dt += time.perf_counter() - t0
@@ -131,7 +132,7 @@ def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
         _log(f"cpu baseline at {th} BLAS threads")
         done, dt, used = _cpu_sample(t, n_sl, min_seconds if th == host else min_seconds / 2, th)
         runs.append({"value": n_amp / (n_sl * dt / done), "cores": used,
-                     "sample": f"{done} of {n_sl} slices timed ({dt:.2f} s)"})
+                     "sample": f"{done} slice contractions of {n_sl} timed ({dt:.2f} s)"})
     best = max(runs, key=lambda r: r["value"])
     return {
         "value": best["value"],
@@ -145,7 +146,8 @@ def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
         "by_threads": runs,
         "sample": (f"oracle = numpy pairwise transpose+matmul executor in complex64 (the GPU dtype) on "
                    f"the {circ_cfg} network, same path/cut/slicing, {n_amp} amplitudes; whole slices timed "
-                   f"and extrapolated linearly to all {n_sl}, at BLAS threads = every host core "
+                   f"(repeated when there are fewer than the time budget needs) and extrapolated linearly to "
+                   f"all {n_sl}, at BLAS threads = every host core "
                    f"({host}) and = 16; value = the faster ({best['cores']} threads: {best['sample']})"),
     }
 
@@ -211,7 +213,22 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
            "step_graphs": d.get("step_graphs"),
            "bound": "latency (2^16-element tensors; ~100 dependent pairwise launches per candidate-step, "
                     "forward + loss + backward replayed as one hipGraph per candidate, SGDG eager; a rank's "
-                    "candidates overlap on their own streams)"}
+                    "candidates overlap on their own streams)",
+           "launches_per_candidate_step": d.get("launches_per_candidate_step"),
+           "algorithmic_bytes_per_candidate_step": d.get("algorithmic_bytes_per_candidate_step")}
+    ab = d.get("algorithmic_bytes_per_candidate_step")
+    if ab:
+        gbs = ab * d["value"] / 1e9
+        out["roofline"] = {"bound": "hbm", "kernel": "every native launch of the training step (aggregate)",
+                           "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                           "achieved_definition": "algorithmic bytes of the step's plans (tq_plan bytes_moved) x "
+                                                  "candidate-steps/s",
+                           "traffic": None}
+    tr = _profile_json("c5_trace_r04.json", "C5")
+    if tr:
+        out["gpu_busy_frac"] = tr.get("gpu_busy_frac")
+        out["trace_launches_per_candidate_step"] = tr.get("launches_per_candidate_step")
+        out["trace_source"] = "profiles/c5_trace_r04.json"
     if "cpu_baseline" in d:
         out["cpu_baseline"] = dict(d["cpu_baseline"], cpu_model=_cpu_model())
     return out
@@ -237,11 +254,15 @@ def other_config(args, cfg: str):
     builds its own plan and arena); the headline stays C4."""
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--steps", str(args.steps),
-           "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
+           "--warmup", str(args.warmup), "--no-c5", "--no-alt", "--no-other",
+           "--cpu-seconds", str(args.other_cpu_seconds)]
+    if args.no_cpu_baseline:
+        cmd.append("--no-cpu-baseline")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
-    return {k: d[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "hbm_kernels") if k in d}
+    return {k: d[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "hbm_kernels", "cpu_baseline",
+                              "plan") if k in d}
 
 
 def launch_ranks(args, argv) -> int:
@@ -281,6 +302,10 @@ def main():
                     help="skip the f32-MFMA GEMM headline (TQ_GEMM_BF16=0, a child process)")
     ap.add_argument("--no-other", action="store_true",
                     help="skip the C2 / C3 secondary lines (child processes, N=1 only)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU-baseline sample budget (seconds of oracle work at every host core)")
+    ap.add_argument("--other-cpu-seconds", type=float, default=4.0,
+                    help="CPU-baseline budget of the C2 / C3 secondary lines")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args, sys.argv[1:]))
@@ -491,7 +516,17 @@ def main():
             "traffic": None,
             "launches_timed": sweep_["launches"],
             "ms_per_step": sweep_["ms"],
+            "algorithmic_bytes_per_step": sweep_["bytes"],
         }
+        pmc_s = _profile_json(f"pmc_{args.config.lower()}_r04.json", args.config)
+        if pmc_s and pmc_s.get("sweep_dispatches"):
+            # HBM bytes of the sweep launches (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC passes of
+            # this command), per launch x this step's launches
+            per = pmc_s["sweep_hbm_bytes"] / pmc_s["sweep_dispatches"]
+            res["roofline"]["traffic"] = per * sweep_["launches"]
+            res["roofline"]["traffic_unit"] = "bytes per step (sweep launches)"
+            res["roofline"]["traffic_vs_algorithmic"] = per * sweep_["launches"] / max(1.0, sweep_["bytes"])
+            res["roofline"]["traffic_source"] = f"profiles/pmc_{args.config.lower()}_r04.json"
     if rank == 0:
         _log("permute probe")
         try:
@@ -501,7 +536,7 @@ def main():
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         _log("cpu baseline")
         try:
-            res["cpu_baseline"] = cpu_baseline(args.config)
+            res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         except Exception as e:  # the baseline must never hide the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
     if world == 1 and rank == 0 and f16 and not args.no_alt:

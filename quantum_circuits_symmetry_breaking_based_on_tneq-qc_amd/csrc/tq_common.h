@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -33,6 +34,27 @@ const std::string& last_error();
       return TQ_ERR_HIP;                                                               \
     }                                                                                  \
   } while (0)
+
+// ---- per-device cache of a launch parameter derived from the device (occupancy caps) -------
+// One slot per (device ordinal, key); 0 = not computed yet.  Concurrent first uses may compute
+// the value twice (the same value) but never race on the slot.
+constexpr int kMaxDevices = 64;
+template <int NKEYS>
+struct DeviceCache {
+  std::atomic<int> v[kMaxDevices][NKEYS] = {};
+  // the cached value of `key` on the current device, computed by `fn()` on first use
+  template <typename F>
+  int get(int key, F&& fn) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return fn();
+    int x = v[dev][key].load(std::memory_order_relaxed);
+    if (x == 0) {
+      x = fn();
+      v[dev][key].store(x, std::memory_order_relaxed);
+    }
+    return x;
+  }
+};
 
 #define TQ_TRY(expr)        \
   do {                      \

@@ -5,8 +5,9 @@
 // (symmetry_breaking_quantum.py:216-230) runs this step on every core after every backward pass;
 // in the reference each core costs ~20 small torch launches (norms, 6 matmuls, an inverse), here the
 // whole group is one launch: one workgroup per parameter, every matrix in LDS (cols <= 32; larger
-// parameters -- a 1-D parameter is 1 x len, a core of bond dimension >= 3 has cols >= 9 ... -- run the
-// same code on a global-memory scratch, `GM`).
+// parameters -- a 1-D parameter is 1 x len, a core of bond dimension >= 3 has cols >= 9 ... -- run on
+// a global-memory scratch, `GM`: when 2 rows < cols in the low-rank Woodbury form, lowrank_step,
+// O(cols^2 rows) work and O(cols rows) scratch; otherwise the dense code below, O(cols^3)).
 //
 // Per parameter (X = the core viewed as row_dim x col_dim = p x n, row-normalised):
 //   Stiefel (p <= n):  V = momentum * buf - g^H;  MX = V X;  W^ = MX - 1/2 X^H X MX;
@@ -78,6 +79,133 @@ __device__ void mm(Cx<R>* C, const Cx<R>* A, int lda, const Cx<R>* B, int ldb, i
     }
     C[i * N + j] = s;
   }
+}
+
+// Stiefel step for p x n parameters with 2p < n (1-D parameters, wide cores): W = W^ - W^^H has
+// rank <= 2p.  With XV = X V (p x p) and U = V - 1/2 X^H XV (n x p), W^ = MX - 1/2 X^H X MX = U X,
+// so W = A B with A = [U | -X^H] (n x 2p) and B = [X ; U^H] (2p x n).  Then (Woodbury)
+//   buf' = W X^H = A (B X^H),   Z = (I + hW) X^H = X^H + h buf',
+//   Y = (I - hW)^-1 Z = Z + h A (I_2p - h B A)^-1 B Z,
+// the same quantities as the dense path (compute_Y, stiefel_optimizer_complex.py:66-74) in
+// O(n^2 p) work (the 1-norm of W, column sums of |A B|) and O(n p) scratch instead of O(n^3) and
+// O(n^2).  The 2p x 2p system is solved with partial pivoting.
+// Scratch (after X p*n | V n*p): U n*p | Z n*p | XV p*p | BX 2p*p | S 2p*(3p) | n reals.
+template <typename T, typename R>
+__device__ void lowrank_step(Cx<R>* X, Cx<R>* V, R lr, T* buf, T* prm, int p, int n) {
+  const int tid = threadIdx.x, q = 2 * p, sa = 3 * p;
+  Cx<R>* U = V + n * p;
+  Cx<R>* Z = U + n * p;
+  Cx<R>* XV = Z + n * p;
+  Cx<R>* BX = XV + p * p;
+  Cx<R>* S = BX + q * p;
+  R* red = reinterpret_cast<R*>(S + q * sa);
+  __shared__ R s_red[kThreads];
+  __shared__ int s_piv;
+  // A[i][c] and B[c][j] read in place from U and X
+  auto Aat = [&](int i, int c) { return c < p ? U[i * p + c] : cx<R>(0) - conj(X[(c - p) * n + i]); };
+  auto Bat = [&](int c, int j) { return c < p ? X[c * n + j] : conj(U[j * p + (c - p)]); };
+  // XV = X V (p x p)
+  mm<R, false, false>(XV, X, n, V, p, p, p, n);
+  __syncthreads();
+  // U = V - 1/2 X^H XV
+  for (int e = tid; e < n * p; e += kThreads) {
+    const int i = e / p, j = e % p;
+    Cx<R> s = cx<R>(0);
+    for (int k = 0; k < p; ++k) s = s + conj(X[k * n + i]) * XV[k * p + j];
+    U[e] = V[e] - R(0.5) * s;
+  }
+  __syncthreads();
+  // ||W||_1 = max_j sum_i |(A B)_ij|
+  R cmax = 0;
+  for (int j = tid; j < n; j += kThreads) {
+    R s = 0;
+    for (int i = 0; i < n; ++i) {
+      Cx<R> w = cx<R>(0);
+      for (int c = 0; c < q; ++c) w = w + Aat(i, c) * Bat(c, j);
+      s += cabs(w);
+    }
+    cmax = s > cmax ? s : cmax;
+  }
+  s_red[tid] = cmax;
+  __syncthreads();
+  for (int w = kThreads / 2; w > 0; w >>= 1) {
+    if (tid < w) s_red[tid] = s_red[tid + w] > s_red[tid] ? s_red[tid + w] : s_red[tid];
+    __syncthreads();
+  }
+  const R nrm = s_red[0];
+  const R t = R(0.5) * R(2) / (nrm + R(1e-8));
+  const R h = (t < lr ? t : lr) / R(2);
+  // BX = B X^H (2p x p)
+  for (int e = tid; e < q * p; e += kThreads) {
+    const int c = e / p, j = e % p;
+    Cx<R> s = cx<R>(0);
+    for (int k = 0; k < n; ++k) s = s + Bat(c, k) * conj(X[j * n + k]);
+    BX[e] = s;
+  }
+  __syncthreads();
+  // buf' = A BX (n x p) -> momentum buffer;  Z = X^H + h buf'
+  for (int e = tid; e < n * p; e += kThreads) {
+    const int i = e / p, j = e % p;
+    Cx<R> s = cx<R>(0);
+    for (int c = 0; c < q; ++c) s = s + Aat(i, c) * BX[c * p + j];
+    st<T, R>(buf, e, s);
+    Z[e] = conj(X[j * n + i]) + h * s;
+  }
+  __syncthreads();
+  // augmented 2p x 3p system [I - h B A | B Z]
+  for (int e = tid; e < q * sa; e += kThreads) {
+    const int c = e / sa, d = e % sa;
+    Cx<R> s = cx<R>(0);
+    if (d < q) {
+      for (int k = 0; k < n; ++k) s = s + Bat(c, k) * Aat(k, d);
+      S[e] = (c == d ? cx<R>(1) : cx<R>(0)) - h * s;
+    } else {
+      for (int k = 0; k < n; ++k) s = s + Bat(c, k) * Z[k * p + (d - q)];
+      S[e] = s;
+    }
+  }
+  __syncthreads();
+  // Gauss-Jordan with partial pivoting (2p rows)
+  for (int k = 0; k < q; ++k) {
+    if (tid == 0) {
+      int best = k;
+      R bv = abs2(S[k * sa + k]);
+      for (int r = k + 1; r < q; ++r) {
+        const R v = abs2(S[r * sa + k]);
+        if (v > bv) { bv = v; best = r; }
+      }
+      s_piv = best;
+    }
+    __syncthreads();
+    const int pr = s_piv;
+    if (pr != k)
+      for (int j = tid; j < sa; j += kThreads) {
+        const Cx<R> a = S[k * sa + j];
+        S[k * sa + j] = S[pr * sa + j];
+        S[pr * sa + j] = a;
+      }
+    __syncthreads();
+    const Cx<R> piv = S[k * sa + k];
+    __syncthreads();
+    for (int j = tid; j < sa; j += kThreads) S[k * sa + j] = cdiv(S[k * sa + j], piv);
+    __syncthreads();
+    for (int e = tid; e < q * sa; e += kThreads) {
+      const int i = e / sa, j = e % sa;
+      if (i != k && j != k) S[e] = S[e] - S[i * sa + k] * S[k * sa + j];
+    }
+    __syncthreads();
+    for (int i = tid; i < q; i += kThreads)
+      if (i != k) S[i * sa + k] = cx<R>(0);
+    __syncthreads();
+  }
+  // Y = Z + h A R (R = the solved right block); parameter <- Y^H
+  for (int64_t e = tid; e < (int64_t)p * n; e += kThreads) {
+    const int r = (int)(e / n), i = (int)(e % n);
+    Cx<R> s = cx<R>(0);
+    for (int c = 0; c < q; ++c) s = s + Aat(i, c) * S[c * sa + q + r];
+    st<T, R>(prm, e, conj(Z[i * p + r] + h * s));
+  }
+  (void)red;
 }
 
 template <typename T, typename R, bool GM>
@@ -166,6 +294,12 @@ __global__ void __launch_bounds__(kThreads) sgdg_kernel(const SgdgLaunch L) {
     V[e] = mom * b - g;
   }
   __syncthreads();
+  if constexpr (GM) {
+    if (2 * p < n) {   // W has rank <= 2p < n: the low-rank (Woodbury) form, O(n^2 p) not O(n^3)
+      lowrank_step<T, R>(X, V, lr, buf, prm, p, n);
+      return;
+    }
+  }
   // 4) MX = V X (n x n);  XMX = X MX (p x n);  XXMX = X^H XMX (n x n) -> W^ = MX - 1/2 XXMX
   mm<R, false, false>(MX, V, p, X, n, n, n, p);
   __syncthreads();
@@ -241,6 +375,19 @@ size_t stiefel_bytes(int p, int n) {
   return cells * sizeof(Cx<R>) + (size_t)std::max(n, p) * sizeof(R) + 16;
 }
 
+// the global-scratch low-rank form (lowrank_step): X p*n | V n*p | U n*p | Z n*p | XV p*p |
+// BX 2p*p | S 2p*3p | n reals
+template <typename R>
+size_t lowrank_bytes(int p, int n) {
+  const size_t cells = (size_t)p * n * 4 + (size_t)p * p + (size_t)2 * p * p + (size_t)6 * p * p;
+  return cells * sizeof(Cx<R>) + (size_t)n * sizeof(R) + 16;
+}
+
+template <typename R>
+size_t global_bytes(int p, int n) {
+  return 2 * p < n ? lowrank_bytes<R>(p, n) : stiefel_bytes<R>(p, n);
+}
+
 template <typename T, typename R>
 int launch_t(const SgdgLaunch& L, hipStream_t stream) {
   int maxn = 1, maxp = 1;
@@ -267,7 +414,7 @@ int launch_t(const SgdgLaunch& L, hipStream_t stream) {
 }  // namespace
 
 size_t sgdg_ws_bytes(int dtype, int rows, int cols) {
-  return (dtype == TQ_F64 || dtype == TQ_C128) ? stiefel_bytes<double>(rows, cols) : stiefel_bytes<float>(rows, cols);
+  return (dtype == TQ_F64 || dtype == TQ_C128) ? global_bytes<double>(rows, cols) : global_bytes<float>(rows, cols);
 }
 
 int sgdg_launch(int dtype, const SgdgLaunch& L, hipStream_t stream) {

@@ -746,17 +746,20 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
   // (r03, same box): C3 1.84 -> 1.27 ms per step (its per-slice launch of 1536 one-chunk
   // workgroups spent ~80 us per round in the store / drain phases, waves waiting 75 %), C4 +-0
   // (13.36 / 13.29 ms; 2 rounds 13.29, 4 rounds 13.24), C3 with 2 rounds 1.56 ms.
-  static const int cap = [] {
+  static const double rounds = [] {
     const char* e = getenv("TQ_S2_CAP");
-    const double rounds = e ? atof(e) : 1.0;   // resident rounds per launch (0 = no cap)
-    if (!(rounds > 0)) return 0;
+    return e ? atof(e) : 1.0;   // resident rounds per launch (0 = no cap)
+  }();
+  // per device (cached; -1 = no cap)
+  static DeviceCache<1> cap_cache;
+  const int cap = !(rounds > 0) ? 0 : std::max(0, cap_cache.get(0, [] {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&sweep2_kernel<T, CB>), NT, 0) != hipSuccess)
-      return 0;
+      return -1;
     return std::max(1, (int)(cus * std::max(1, per) * rounds));
-  }();
+  }));
   if (cap > 0 && blocks > cap) {
     S2Launch R = L;
     int b = 0;

@@ -280,15 +280,17 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
   }
 #undef TQ_SD_FN
 #undef TQ_SD_MIX
-  static int slots[(kS2DMaxTin + 1) * 32] = {};
+  // resident workgroups of this instantiation on the current device (cached per device)
+  static DeviceCache<(kS2DMaxTin + 1) * 32> slot_cache;
   const int key = ta * 32 + tb;
-  if (!slots[key]) {
+  const int slots = slot_cache.get(key, [&] {
     int dev = 0, cus = 0, per = 0;
-    TQ_HIP(hipGetDevice(&dev));
-    TQ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    TQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kWaves, 0));
-    slots[key] = std::max(1, cus * std::max(1, per));
-  }
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 64 * kWaves, 0) != hipSuccess)
+      return 256;
+    return std::max(1, cus * std::max(1, per));
+  });
   S2DLaunch R = L;
   static const int diag = [] {
     const char* e = getenv("TQ_S2D_DIAG");
@@ -296,7 +298,7 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
   }();
   int blocks = 0;
   for (int q = 0; q < R.nops; ++q) {
-    const int want = std::max(1, slots[key] / R.nops);
+    const int want = std::max(1, slots / R.nops);
     R.op[q].nblocks = std::max(1, std::min(R.op[q].nblocks, want));
     R.op[q].block_begin = blocks;
     R.op[q].pad = diag;

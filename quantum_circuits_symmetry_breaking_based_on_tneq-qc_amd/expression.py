@@ -231,15 +231,17 @@ class HipContractExpression:
             total = torch.zeros(self.out_shape, dtype=dt, device=dev)
         return total
 
-    def reverse_tree(self) -> "_ReverseTree":
-        """The per-step forward / gradient expressions used by autograd (built once)."""
-        rev = self._plans.get("reverse")
+    def reverse_tree(self, dtype: torch.dtype = torch.complex64) -> "_ReverseTree":
+        """The per-step forward / gradient expressions used by autograd (built once per dtype:
+        the in-place mode orders are chosen from that dtype's step plans)."""
+        key = ("reverse", dtype)
+        rev = self._plans.get(key)
         if rev is None:
             with self._lock:
-                rev = self._plans.get("reverse")
+                rev = self._plans.get(key)
                 if rev is None:
-                    rev = _ReverseTree(self)
-                    self._plans["reverse"] = rev
+                    rev = _ReverseTree(self, dtype)
+                    self._plans[key] = rev
         return rev
 
     def grad_expression(self, i: int) -> Tuple["HipContractExpression", List[int]]:
@@ -355,10 +357,10 @@ def _in_place_order(mi, mj, res, ext):
     return tuple(out) if set(out) == keep and len(out) == len(keep) else None
 
 
-def _writes_through_permute(e: "HipContractExpression") -> bool:
-    """True when the step's plan ends with a permute of its result into the requested order."""
-    p = NativePlan(e.net, e.path, torch.complex64, None, [])
-    return "result->out" in p.describe()
+def _writes_through_permute(e: "HipContractExpression", dtype: torch.dtype) -> bool:
+    """True when the step's plan for `dtype` ends with a permute of its result into the
+    requested order (the plan is kept: the runtime of that dtype reuses it)."""
+    return "result->out" in e.plan(dtype).describe()
 
 
 class _ReverseTree:
@@ -380,7 +382,10 @@ class _ReverseTree:
     its parameters in place), the whole forward / backward launch sequence is captured once into
     a hipGraph (torch.cuda.CUDAGraph) and replayed."""
 
-    def __init__(self, expr: "HipContractExpression"):
+    _MAX_RUNTIMES = 4   # per tree: (device, stream) pairs kept, least recently used dropped
+
+    def __init__(self, expr: "HipContractExpression", dtype: torch.dtype = torch.complex64):
+        self.dtype = dtype
         net = expr.net
         sym = net.symbols
         st = _State(net)
@@ -408,7 +413,7 @@ class _ReverseTree:
                 if nat is not None and nat != tuple(res):
                     cand = HipContractExpression(f"{s2(mi)},{s2(mj)}->{s2(nat)}", shp(mi), shp(mj),
                                                  optimize=[(0, 1)])
-                    if not _writes_through_permute(cand):
+                    if not _writes_through_permute(cand, dtype):
                         fwd, res = cand, nat
             self.modes[k] = tuple(res)
             if fwd is None:
@@ -437,7 +442,7 @@ class _ReverseTree:
                     nat = _in_place_order(hk, m_o, m_a, ext)
                     if nat is not None and nat != tuple(m_a):
                         cand = HipContractExpression(",".join(terms) + "->" + s2(nat), *shapes, optimize=path)
-                        if not _writes_through_permute(cand):
+                        if not _writes_through_permute(cand, dtype):
                             g, h_a = cand, nat
                 if g is None:
                     g = HipContractExpression(",".join(terms) + "->" + s2(m_a), *shapes, optimize=path)
@@ -453,10 +458,16 @@ class _ReverseTree:
         self._rt: Dict[tuple, "_TreeRuntime"] = {}
 
     def runtime(self, dtype, device) -> "_TreeRuntime":
+        """The static buffers / graphs of (dtype, device, current stream), a bounded LRU: each
+        graphs.capture_step call brings a new stream, so older runtimes are dropped (a backward
+        still holding one keeps it alive through its autograd context)."""
         key = (dtype, device.index, torch.cuda.current_stream(device).cuda_stream)
-        rt = self._rt.get(key)
+        rt = self._rt.pop(key, None)
         if rt is None:
-            rt = self._rt[key] = _TreeRuntime(self, dtype, device)
+            rt = _TreeRuntime(self, dtype, device)
+            while len(self._rt) >= self._MAX_RUNTIMES:
+                self._rt.pop(next(iter(self._rt)))
+        self._rt[key] = rt
         return rt
 
 
@@ -596,16 +607,17 @@ class _HipContractFn(torch.autograd.Function):
         ts = [t.detach() if isinstance(t, torch.Tensor) else torch.as_tensor(t) for t in tensors]
         ctx.expr = expr
         ctx.in_meta = [(t.dtype, t.device, tuple(t.shape)) for t in ts]
-        rev = expr.reverse_tree()
+        dt = ts[0].dtype
+        for t in ts[1:]:
+            dt = torch.promote_types(dt, t.dtype)
+        ctx.dt = dt
+        rev = expr.reverse_tree(dt)
         with torch.no_grad():
             if rev.single is not None:
                 ctx.save_for_backward(*ts)
                 return expr._forward(*ts)
             dev = next((t.device for t in ts if t.device.type == "cuda"),
                        torch.device("cuda", torch.cuda.current_device()))
-            dt = ts[0].dtype
-            for t in ts[1:]:
-                dt = torch.promote_types(dt, t.dtype)
             dtype_code(dt)
             ins = [t.to(device=dev, dtype=dt).resolve_conj().resolve_neg().contiguous() for t in ts]
             for t, shp in zip(ins, expr.shapes):
@@ -623,7 +635,7 @@ class _HipContractFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         expr = ctx.expr
-        rev = expr.reverse_tree()
+        rev = expr.reverse_tree(ctx.dt)
         needs = list(ctx.needs_input_grad[1:])
         if rev.single is not None:
             (t,) = ctx.saved_tensors

@@ -129,6 +129,29 @@ def gpu_step(target, cands, streams=None, graphs=None):
     return losses
 
 
+def launch_stats(cands, dtype=torch.complex128):
+    """Per candidate-step: kernel launches and algorithmic HBM bytes of the native plans the
+    graphed step replays (the reverse tree's forward step plans, every gradient step plan, one
+    SGDG launch), from the plans' own counters (tq_plan_query n_launch_* / bytes_moved).  The
+    fidelity loss's few torch kernels are not counted."""
+    launches, nbytes, n_plans = [], [], []
+    for expr, params, _, _, _, _ in cands:
+        rev = expr.reverse_tree(dtype)
+        L, B, n = 1, 0, 0                       # + the SGDG launch
+        for (i, j, k, fwd, bwd) in rev.steps:
+            plans = [fwd.plan(dtype)] + [g.plan(dtype) for (_, _, g, _) in bwd]
+            for pl in plans:
+                L += pl.query("n_launch_once") + pl.query("n_launch_slice")
+                B += pl.query("bytes_moved")
+                n += 1
+        launches.append(L)
+        nbytes.append(B)
+        n_plans.append(n)
+    return {"launches_per_candidate_step": sum(launches) / len(launches),
+            "algorithmic_bytes_per_candidate_step": sum(nbytes) / len(nbytes),
+            "plans_per_candidate": sum(n_plans) / len(n_plans)}
+
+
 def _log(msg):
     print(f"[c5_bench] {msg}", file=sys.stderr, flush=True)
 
@@ -255,6 +278,10 @@ def main():
            "host_issue_ms_per_step": [float(t[2]) / a.steps * 1e3 for t in allt],
            "wall_ms_per_step_per_rank": [float(t[1]) / a.steps * 1e3 for t in allt],
            "loss_after": [my_losses[k] for k in sorted(my_losses)]}
+    try:
+        res.update(launch_stats(cands))
+    except Exception as e:  # the stats must never hide the timing
+        res["launch_stats_error"] = repr(e)
     if world > 1:
         dist.destroy_process_group()
     if rank != 0:

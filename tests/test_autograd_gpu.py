@@ -107,7 +107,7 @@ def test_repeated_steps_hit_the_captured_graph_and_stay_exact(dev):
             for p_, c_, a_ in zip(pg, pc, gc):
                 p_.mul_(0.9).add_(0.01 * a_.to("cuda"))
                 c_.mul_(0.9).add_(0.01 * a_)
-    rt = expr.reverse_tree().runtime(torch.complex128, pg[0].device)
+    rt = expr.reverse_tree(torch.complex128).runtime(torch.complex128, pg[0].device)
     assert len(rt.graphs) >= 2       # forward and backward captured
     # two forwards, then the first backward: recomputed from its own inputs
     x1 = [p.detach().clone().requires_grad_(True) for p in pg]
