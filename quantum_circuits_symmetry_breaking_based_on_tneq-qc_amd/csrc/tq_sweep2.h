@@ -175,6 +175,7 @@ struct S2DOp {
   double beta = 0.0;
   uint32_t* amax = nullptr;        // as S2Op::amax
   const int32_t* split_sc = nullptr;  // as S2Op::split_sc
+  int order = 0, pad2 = 0;         // tile order (tq_sweepd.hip): 0 grid-strided, 1 blocked
 };
 struct S2DLaunch {
   int nops = 0, pad = 0;

@@ -164,7 +164,18 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
       else if (w.x == 12345.f) *p = w;
     }
   };
-  for (int64_t t = (int64_t)((int)blockIdx.x - op.block_begin) * kWaves + wave; t < ntiles; t += nw) {
+  // tile order: grid-strided (default: concurrently running workgroups write neighbouring 1-KiB
+  // pieces of the same output rows) or blocked (op.order == 1, TQ_S2D_BLOCKED=1: each workgroup
+  // walks its own contiguous range of tiles, i.e. whole runs of one row set)
+  const int64_t blk = (int)blockIdx.x - op.block_begin;
+  int64_t t0 = blk * kWaves + wave, t_end = ntiles, t_step = nw;
+  if (op.order == 1) {
+    const int64_t per = ((ntiles + op.nblocks - 1) / op.nblocks + kWaves - 1) / kWaves * kWaves;
+    t0 = blk * per + wave;
+    t_end = ntiles < (blk + 1) * per ? ntiles : (blk + 1) * per;
+    t_step = kWaves;
+  }
+  for (int64_t t = t0; t < t_end; t += t_step) {
     // column tile t: columns 32t .. 32t+31 (bits 0..4 = lane, bit 5 = t & 1, bits >= 6: tables)
     const int64_t g = t >> 1;
     const int cl = (int)(t & 1) * 32 + fr;
@@ -251,6 +262,10 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     const char* e = getenv("TQ_S2D_NT");
     return e && e[0] == '1';
   }();
+  static const int order = [] {
+    const char* e = getenv("TQ_S2D_BLOCKED");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
   if (tb > ta) std::swap(ta, tb);
   auto pow2tin = [](int t) { return t == 2 || t == 4 || t == 8 || t == 16; };
   if (!pow2tin(ta) || (tb && !pow2tin(tb))) {
@@ -302,6 +317,7 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     R.op[q].nblocks = std::max(1, std::min(R.op[q].nblocks, want));
     R.op[q].block_begin = blocks;
     R.op[q].pad = diag;
+    R.op[q].order = order;
     blocks += R.op[q].nblocks;
   }
   hipLaunchKernelGGL(reinterpret_cast<void (*)(S2DLaunch)>(const_cast<void*>(fn)), dim3(blocks), dim3(64 * kWaves), 0,

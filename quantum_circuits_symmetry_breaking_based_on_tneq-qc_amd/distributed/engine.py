@@ -133,6 +133,7 @@ class DistributedEngineSiamese:
         self._local_qctn: Optional[_LocalQCTN] = None
         self._contract_plan: Optional[DistributedContractPlan] = None
         self._jobs: Dict[tuple, tuple] = {}
+        self._last_job = None
 
     # ---------------------------------------------------------------- proxies (:334-365)
     @property
@@ -334,7 +335,11 @@ class DistributedEngineSiamese:
         if not mine:   # an empty partition still needs a dtype / device to build its scalar 1
             ref = next(iter(cores.values()))
             ops[0] = ref.tensor if isinstance(ref, TNTensor) else ref
+        if not mine and torch.is_grad_enabled():
+            # an empty partition joins the backward through TreeContraction.leaf
+            ops[0] = ops[0].detach().requires_grad_() if not ops[0].requires_grad else ops[0]
         res = job(*ops)
+        self._last_job = job
         if isinstance(res, TNTensor):
             if res.tensor.is_complex():
                 return TNTensor(res.tensor.abs() ** 2, res.scale, res.log_scale)
@@ -347,7 +352,7 @@ class DistributedEngineSiamese:
         """(loss, grads of the local partition's cores) with the reference's cross-entropy loss
         -mean(target * (log(clamp(P, 1e-10)) + log_scale)) (:1986-2019)."""
         raws = []
-        for name in self._local_qctn.cores:
+        for name in (self._local_qctn.cores if self._local_qctn is not None else []):
             w = self._local_qctn.cores_weights[name]
             t = w.tensor if isinstance(w, TNTensor) else w
             t.requires_grad_(True)
@@ -356,7 +361,9 @@ class DistributedEngineSiamese:
             raws.append(t)
         result = self.contract_distributed(circuit_states_list, measure_input_list, measure_is_matrix)
         loss = self._compute_cross_entropy_loss(result, target)
-        grads = torch.autograd.grad(loss, raws, allow_unused=True)
+        job = self._last_job
+        extra = [job.leaf] if job is not None and job.leaf is not None else []   # an empty partition
+        grads = torch.autograd.grad(loss, raws + extra, allow_unused=True)[:len(raws)]
         return loss, [torch.zeros_like(t) if g is None else g.contiguous() for g, t in zip(grads, raws)]
 
     @staticmethod

@@ -85,7 +85,11 @@ class TreeContraction:
     `executor(eq, shapes, operands, slices, slice_range)` contracts one (sub-)network and
     defaults to the native plan (HipContractExpression); CPU tests inject the oracle (or, for
     gradients, a differentiable torch executor).  Operands may be TNTensors: their scales are
-    carried as log-scales through the stages and the result is a TNTensor."""
+    carried as log-scales through the stages and the result is a TNTensor.
+
+    Gradients: every rank must run its backward (the stage adjoints are collectives); a rank
+    whose partition is empty differentiates w.r.t. `self.leaf` (its scalar 1), since
+    torch.autograd.grad only runs the nodes on a path to the requested inputs."""
 
     def __init__(self, eq: str, shapes: Sequence[Sequence[int]], group=None,
                  partitions: Optional[Sequence[Sequence[int]]] = None,
@@ -190,7 +194,11 @@ class TreeContraction:
                 sign = -sign if o.scale < 0 else sign
                 o = o.tensor
             raw.append(o)
-        grad = torch.is_grad_enabled() and any(getattr(o, "requires_grad", False) for o in raw)
+        # autograd when an operand requires grad (an empty partition looks at every operand it
+        # was given: its rank still has to run the stage adjoints in backward)
+        pool = raw if mine else [o.tensor if isinstance(o, TNTensor) else o for o in operands if o is not None]
+        grad = torch.is_grad_enabled() and any(getattr(o, "requires_grad", False) for o in pool)
+        self.leaf = None
         if self.world > 1 and not self._warm:
             _first_use(ref, self.group)
             self._warm = True
@@ -200,7 +208,10 @@ class TreeContraction:
         else:   # more ranks than operands: an empty partition is the scalar 1
             cur = torch.ones((), dtype=ref.dtype, device=ref.device)
             if grad:
+                # the rank's backward must reach the stage Functions: differentiate w.r.t. this
+                # leaf (torch.autograd.grad only runs the nodes on a path to its inputs)
                 cur.requires_grad_()
+                self.leaf = cur
         if sign < 0:
             cur = -cur
         for row in self.stages:
@@ -228,6 +239,10 @@ class TreeContraction:
                 left, right, log_l, log_r = _blocks(cur, rec, logs)
                 part = self._contract(("stage", st.s, st.g), st.eq, st.shapes, [left, right],
                                       st.slice_syms, (pos, None, G))
+                if grad and not part.requires_grad:
+                    # a member without a K shard (fewer slices than members) still runs the
+                    # stage adjoints in backward: keep its zero partial on the graph
+                    part = part + 0 * sum(x.sum() for x in (left, right) if x.requires_grad)
                 # sum of the members' K-shard partials (allreduce_grad.py:13-60), in member
                 # order, log-scales aligned to the max (distributed_engine.py:1462-1472)
                 pair = log_l + log_r

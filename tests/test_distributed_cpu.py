@@ -168,3 +168,46 @@ def test_two_rank_slice_gradients_and_scales():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     for rank, err_out, err_g, err_tn, is_tn in sorted(q.get(timeout=5) for _ in range(2)):
         assert err_out < 1e-12 and err_g < 1e-10 and err_tn < 1e-12 and is_tn, (rank, err_out, err_g, err_tn)
+
+
+def _few_slices_worker(rank, world, port, q):
+    """More ranks than slices (3 ranks, 2 slices): the rank without a slice still joins the
+    backward's collectives with a zero partial; gradients are world x the single-process ones."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task
+    from tneq_qc_amd.distributed import SlicedContraction
+    task = amplitude_task(BrickWall(8, 4, 2), list(range(2, 6)), cut=4, n_slice=1)
+
+    class _Expr:
+        n_slices = 2 ** len(task.sliced)
+        out_shape = (2,) * len(task.open_qubits)
+
+    def executor(rng, out, *tensors):
+        return _torch_slices(task.eq, task.sliced, rng, tensors)
+
+    job = SlicedContraction(_Expr(), executor=executor)
+    ts = [torch.tensor(o, dtype=torch.complex128, requires_grad=True) for o in task.operands]
+    res = job(*ts)
+    g = torch.autograd.grad((res.abs() ** 2).sum(), ts)
+    rts = [torch.tensor(o, dtype=torch.complex128, requires_grad=True) for o in task.operands]
+    ref = torch.einsum(task.eq, *rts)
+    rg = torch.autograd.grad((ref.abs() ** 2).sum(), rts)
+    err = max(float((a - world * b).abs().max()) for a, b in zip(g, rg)) / max(float(b.abs().max()) for b in rg)
+    q.put((rank, float((res.detach() - ref.detach()).abs().max()), err))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_more_ranks_than_slices_gradients():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_few_slices_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, e_out, e_g in sorted(q.get(timeout=5) for _ in range(3)):
+        assert e_out < 1e-12 and e_g < 1e-10, (rank, e_out, e_g)

@@ -24,8 +24,11 @@ def _free_port():
 def _oracle_executor(eq, shapes, operands, slices, slice_range):
     from oracle.contract_ref import contract, sliced_operands
     arrs = [o.numpy() for o in operands]
-    if not slices:
-        return torch.from_numpy(np.ascontiguousarray(contract(eq, *arrs)))
+    if not slices:   # one slice: only range member 0 contracts it (as the native path)
+        r = contract(eq, *arrs)
+        if slice_range is not None and slice_range[0] >= 1:
+            r = np.zeros_like(r)
+        return torch.from_numpy(np.ascontiguousarray(r))
     lhs = eq.split("->")[0].split(",")
     ext = {}
     for t, a in zip(lhs, arrs):
@@ -140,8 +143,9 @@ def _torch_executor(eq, shapes, operands, slices, slice_range):
     views (the same slice enumeration as tq_plan_execute: row-major over `slices`)."""
     lhs, rhs = eq.split("->")
     terms = lhs.split(",")
-    if not slices:
-        return torch.einsum(eq, *operands)
+    if not slices:   # one slice: only range member 0 contracts it (as the native path)
+        r = torch.einsum(eq, *operands)
+        return r if slice_range is None or slice_range[0] < 1 else torch.zeros_like(r)
     ext = {}
     for t, o in zip(terms, operands):
         for c, e in zip(t, o.shape):
@@ -262,3 +266,44 @@ def test_tree_contraction_tntensor_scales(world):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     for rank, err in sorted(q.get(timeout=5) for _ in range(world)):
         assert err < 1e-12, (rank, err)
+
+
+def _empty_part_worker(rank, world, port, q):
+    """More ranks than operands (4 ranks, 3 operands): the empty partition is the scalar 1, its
+    rank still takes part in every stage and in the backward."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tneq_qc_amd.distributed import TreeContraction
+        rng = np.random.default_rng(1)
+        eq = "ab,bc,cd->ad"
+        shapes = [(3, 4), (4, 5), (5, 2)]
+        arrs = [rng.standard_normal(s) + 1j * rng.standard_normal(s) for s in shapes]
+        job = TreeContraction(eq, shapes, executor=_torch_executor)
+        ts = [torch.tensor(a, requires_grad=True) for a in arrs]
+        out = job(*ts)
+        extra = [job.leaf] if job.leaf is not None else []
+        g = torch.autograd.grad((out.abs() ** 2).sum(), ts + extra, allow_unused=True)
+        assert (job.leaf is not None) == (not job.parts[rank])
+        rts = [torch.tensor(a, requires_grad=True) for a in arrs]
+        ref = torch.einsum(eq, *rts)
+        rg = torch.autograd.grad((ref.abs() ** 2).sum(), rts)
+        errs = [float((g[t] - world * rg[t]).abs().max() / rg[t].abs().max()) for t in job.parts[rank]]
+        q.put((rank, float((out.detach() - ref.detach()).abs().max()), max(errs) if errs else 0.0))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tree_gradients_with_an_empty_partition():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_part_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, e_out, e_g in sorted(q.get(timeout=5) for _ in range(4)):
+        assert e_out < 1e-12 and e_g < 1e-10, (rank, e_out, e_g)
