@@ -98,7 +98,7 @@ __device__ void lowrank_step(Cx<R>* X, Cx<R>* V, R lr, T* buf, T* prm, int p, in
   Cx<R>* XV = Z + n * p;
   Cx<R>* BX = XV + p * p;
   Cx<R>* S = BX + q * p;
-  R* red = reinterpret_cast<R*>(S + q * sa);
+  R* red = reinterpret_cast<R*>(S + q * sa);   // (== the caller's `red`: X + 4pn + 9p^2)
   __shared__ R s_red[kThreads];
   __shared__ int s_piv;
   // A[i][c] and B[c][j] read in place from U and X
@@ -250,7 +250,11 @@ __global__ void __launch_bounds__(kThreads) sgdg_kernel(const SgdgLaunch L) {
   Cx<R>* T1 = MX + n * n;
   Cx<R>* W = T1 + p * n;
   Cx<R>* A = W + n * n;      // n x (n + p) augmented system
-  R* red = reinterpret_cast<R*>(A + n * (n + p));   // n reals of scratch
+  // n reals of scratch: at the end of the layout the step uses (the low-rank form's scratch is
+  // O(n p): the dense layout's offsets lie far beyond it)
+  const bool lowrank = GM && 2 * p < n;
+  R* red = lowrank ? reinterpret_cast<R*>(X + (size_t)p * n * 4 + (size_t)p * p * 9)
+                   : reinterpret_cast<R*>(A + n * (n + p));
   const int na = n + p;
   // 1) X = unit(P): rows divided by (row 2-norm + 1e-8)           gutils.py:7-9
   for (int64_t i = tid; i < numel; i += kThreads) X[i] = ld<T, R>(prm, i);
@@ -295,7 +299,7 @@ __global__ void __launch_bounds__(kThreads) sgdg_kernel(const SgdgLaunch L) {
   }
   __syncthreads();
   if constexpr (GM) {
-    if (2 * p < n) {   // W has rank <= 2p < n: the low-rank (Woodbury) form, O(n^2 p) not O(n^3)
+    if (lowrank) {   // W has rank <= 2p < n: the low-rank (Woodbury) form, O(n^2 p) not O(n^3)
       lowrank_step<T, R>(X, V, lr, buf, prm, p, n);
       return;
     }

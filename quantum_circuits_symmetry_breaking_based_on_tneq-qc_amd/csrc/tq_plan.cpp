@@ -938,7 +938,7 @@ class Compiler {
   static int slice_lanes() {
     static const int v = [] {
       const char* e = getenv("TQ_SLICE_LANES");
-      return e ? std::max(1, std::min(16, atoi(e))) : 16;
+      return e ? std::max(1, std::min(64, atoi(e))) : 16;
     }();
     return v;
   }

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 OUT=gpurun_out/knobs.jsonl
-for KV in "BASE=1" "TQ_S2D_BLOCKED=1" "TQ_S2D_NT=1" "TQ_S2_B4MIN=4096" "TQ_S2_B4MIN=2048" "TQ_S2_BLOCKS=0" "TQ_S2_EPI=0" "TQ_S2_MINLC=1"; do
+for KV in "BASE=1" "TQ_SLICE_LANES=32" "TQ_S2D_BLOCKED=1" "TQ_S2D_NT=1" "TQ_S2_B4MIN=4096" "TQ_S2_B4MIN=2048" "TQ_S2_BLOCKS=0" "TQ_S2_EPI=0" "TQ_S2_MINLC=1"; do
   echo "== $KV"
   r=$(env $KV timeout -k 10 120 python3 scripts/rank_sim.py C4 2>/dev/null | tail -1) || exit 1
   echo "{\"knob\": \"$KV\", \"what\": \"C4 ranks\", \"res\": $r}" >> $OUT
