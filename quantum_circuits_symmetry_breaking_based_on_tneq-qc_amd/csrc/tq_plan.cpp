@@ -924,8 +924,10 @@ class Compiler {
     }();
     return v;
   }
-  // slices per batch when the per-slice working set is small (TQ_SLICE_LANES, default 16; 1 = off;
-  // C3 with the capped sweep2 launches: 1.27 ms per step at 8 lanes, 1.18 at 16)
+  // slices per batch when the per-slice working set is small (TQ_SLICE_LANES, default 32; 1 = off;
+  // C3 with the capped sweep2 launches: 1.27 ms per step at 8 lanes, 1.18 at 16; r04 with 32-op
+  // sweep2 launches: 0.778 -> 0.726 ms at 32 (two launches per per-slice level, half the GEMM /
+  // reduce / permute batches), profiles/knobs_r04.jsonl)
   // arena the lane copies may add in total (TQ_LANE_ARENA_MB, default 6 GiB of the 288 GB):
   // C3's 6-MiB per-slice part gets 16 lanes, C4's 1.1 GiB gets 4 (measured: 16.4 -> 15.9 ms/step)
   static size_t lane_arena_budget() {
@@ -938,14 +940,17 @@ class Compiler {
   static int slice_lanes() {
     static const int v = [] {
       const char* e = getenv("TQ_SLICE_LANES");
-      return e ? std::max(1, std::min(64, atoi(e))) : 16;
+      return e ? std::max(1, std::min(64, atoi(e))) : 32;
     }();
     return v;
   }
-  static int s2_min_logc() {   // narrowest chunk (log2 columns) of the small-tensor rule
+  // narrowest chunk (log2 columns) of the small-tensor rule (TQ_S2_MINLC; 1 since r04: with the
+  // 32-lane batches and 4096-element register-block tiles C2 0.399 -> 0.365 ms, C3 0.786 ->
+  // 0.700, C4 N = 8 rank 2.21 -> 2.12, profiles/knobs_r04.jsonl; r03 measured 2 better alone)
+  static int s2_min_logc() {
     static const int v = [] {
       const char* e = getenv("TQ_S2_MINLC");
-      return e ? std::max(0, std::min(5, atoi(e))) : 2;
+      return e ? std::max(0, std::min(5, atoi(e))) : 1;
     }();
     return v;
   }
@@ -1212,10 +1217,11 @@ class Compiler {
     // register blocks of consecutive square gates (S2Desc::pmeta): the pass starting at gate j
     // ends before block_span(j, ng); bm = its block positions, live = the live positions
     // TQ_S2_B4MIN: the smallest tile (elements) that gets 16-element register blocks (default
-    // 8192: every thread busy; smaller tiles leave threads idle in the block passes)
+    // 4096 since r04: a 4096-element tile then leaves half the threads idle in its block passes,
+    // but needs fewer passes -- C2 0.386 -> 0.370 ms, C4 N = 8 rank -0.3 %; 8192 before)
     static const int64_t b4min = [] {
       const char* e = getenv("TQ_S2_B4MIN");
-      return e ? (int64_t)atoll(e) : (int64_t)8192;
+      return e ? (int64_t)atoll(e) : (int64_t)4096;
     }();
     const int64_t tile_elems = int64_t(1) << (lc + used);
     const int B = (P_.esz <= 8 && tile_elems >= b4min) ? 4 : s2_block_bits((int)P_.esz, tile_elems);

@@ -10,7 +10,7 @@ seconds and through size-independent properties where it does not.
   Componentwise (the Gauss-3M imaginary part): every amplitude with
   |amp| >= 1e-2 max|amp| within 2e-3 relative, the normwise bound carried down to it.
 * C3 / C4 whole job EXACTLY as bench.py launches it (SlicedContraction at world 1 over the full
-  slice range: C4 4 slice lanes / C3 16, the lane-batched f16-split boundary GEMM with per-lane
+  slice range: C4 4 slice lanes / C3 32, the lane-batched f16-split boundary GEMM with per-lane
   operand-max words, lane_sum, lane-merged sweep launches, the captured hipGraph replayed)
   against the oracle's sum over all slices (oracle.contract_ref.contract_sliced; the partial sums
   the reference reduces at distributed_engine.py:1477-1497).
@@ -122,7 +122,7 @@ def _production_plan_checks(e, cfg, lanes):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cfg,lanes", [("C3", 16), ("C4", 4)])
+@pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 4)])
 def test_bench_launch_vs_oracle(dev, cfg, lanes):
     import torch
     from tneq_qc_amd.circuits import config_task
@@ -146,7 +146,7 @@ def test_bench_launch_vs_oracle(dev, cfg, lanes):
     assert np.array_equal(res[1], res[2])   # replays are deterministic
 
 
-@pytest.mark.parametrize("cfg,lanes", [("C3", 16), ("C4", 4)])
+@pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 4)])
 def test_lane_skew_per_lane_scales(dev, cfg, lanes):
     import torch
     from tneq_qc_amd.circuits import config_task

@@ -228,10 +228,10 @@ def test_boundary_gemm_takes_presplit_operands(cfg):
 
 def test_slice_lanes_within_the_arena_budget():
     """Slices run in batches of `lanes` (a power of two) within an arena budget (C3: 64
-    latency-bound slices, 8 per batch, each lane with its own copy of the per-slice buffers);
+    latency-bound slices, 32 per batch, each lane with its own copy of the per-slice buffers);
     C4's 1.1-GiB per-slice part gets 4 (the lane copies stay within 6 GiB; tq_plan.cpp, Plan::lanes)."""
     e3, p3 = _plan(config_task("C3"))
-    assert p3.query("lanes") == 16
+    assert p3.query("lanes") == 32
     e4, p4 = _plan(config_task("C4"))
     assert p4.query("lanes") == 4   # 1.1-GiB per-slice part: 4 lanes in the 6-GiB budget
     e2, p2 = _plan(config_task("C2"))
