@@ -1430,9 +1430,24 @@ class Compiler {
         for (int q = j; q < e; ++q) {
           const S2Gate& G = d.gate[q];
           // index bit t of the gate <-> position of input k = 1 << t
-          const int i0 = local(__builtin_ctz((uint32_t)kdep[q][1]));
+          int i0 = local(__builtin_ctz((uint32_t)kdep[q][1]));
           int code = i0;
-          if (G.K == 4) code |= (local(__builtin_ctz((uint32_t)kdep[q][2])) << 2) | 16;
+          if (G.K == 4) {
+            int j0 = local(__builtin_ctz((uint32_t)kdep[q][2]));
+            if (i0 > j0) {
+              // canonical placement I < J: swap the gate's two legs -- input / output index bits
+              // 0 and 1 of every coefficient (a square gate: its outputs sit on its inputs'
+              // positions).  The kernel then needs 6 (B = 4) / 3 (B = 3) block-gate bodies
+              // instead of 12 / 6 (instruction-cache footprint, tq_sweep2.hip blk_gate)
+              uint8_t cg[16];
+              auto sw = [](int v) { return ((v & 1) << 1) | ((v >> 1) & 1); };
+              for (int k = 0; k < 4; ++k)
+                for (int n = 0; n < 4; ++n) cg[sw(k) * 4 + sw(n)] = d.cgidx[q][k * 4 + n];
+              for (int t = 0; t < 16; ++t) d.cgidx[q][t] = cg[t];
+              std::swap(i0, j0);
+            }
+            code = i0 | (j0 << 2) | 16;
+          }
           pm[kS2PmCode + (q - j)] = code;
         }
         group_lut(live & ~bm, d.k.lut[j]);

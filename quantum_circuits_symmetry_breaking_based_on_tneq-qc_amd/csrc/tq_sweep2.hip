@@ -302,16 +302,16 @@ template <typename T, int B>
 __device__ __forceinline__ void blk_gate(T (&x)[1 << B], const T* cf, int code) {
 #define TQ_B4(i, j) case 16 | (j << 2) | i: blk_apply4<T, B, i, j>(x, cf); break;
 #define TQ_B2(i) case i: blk_apply2<T, B, i>(x, cf); break;
+  // the plan compiler emits I < J only (it swaps a gate's legs otherwise): 6 / 3 bodies
   if constexpr (B == 4) {
     switch (code) {
-      TQ_B4(0, 1) TQ_B4(0, 2) TQ_B4(0, 3) TQ_B4(1, 0) TQ_B4(1, 2) TQ_B4(1, 3)
-      TQ_B4(2, 0) TQ_B4(2, 1) TQ_B4(2, 3) TQ_B4(3, 0) TQ_B4(3, 1) TQ_B4(3, 2)
+      TQ_B4(0, 1) TQ_B4(0, 2) TQ_B4(0, 3) TQ_B4(1, 2) TQ_B4(1, 3) TQ_B4(2, 3)
       TQ_B2(0) TQ_B2(1) TQ_B2(2) TQ_B2(3)
       default: break;
     }
   } else {
     switch (code) {
-      TQ_B4(0, 1) TQ_B4(0, 2) TQ_B4(1, 0) TQ_B4(1, 2) TQ_B4(2, 0) TQ_B4(2, 1)
+      TQ_B4(0, 1) TQ_B4(0, 2) TQ_B4(1, 2)
       TQ_B2(0) TQ_B2(1) TQ_B2(2)
       default: break;
     }
@@ -631,8 +631,10 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     const int64_t base = base_out(i, ch);
     // the tile leaves LDS in batches of 4 register slots, each batch stored before the next is
     // read (keeps the register budget)
-    auto store_chunk = [&](auto tracked) {
-      constexpr bool TRK = decltype(tracked)::value;
+    // the max of the stored values is always tracked (3 VALU per complex64 element; the atomic
+    // only runs for an S2Op::amax): one instantiation of each store form instead of two, the
+    // code sits in the 64-KB instruction cache two CUs share (r04: -9 KB of 72)
+    auto store_chunk = [&]() {
       if (rout >= 4) {
         for (int r0 = 0; r0 < rout; r0 += 4) {
           T t[4];
@@ -644,7 +646,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
               T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + q]), sto);
               const T v = use_beta ? scale_add(t[q], *p, beta) : t[q];
               TQ_ST(p, stored(v));
-              if constexpr (TRK) track(v);
+              track(v);
             }
           }
           asm volatile("" ::: "memory");
@@ -657,7 +659,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
             T* p = lane_at(Y + uniform(base + keep.st_hm[r]), sto);
             const T v = use_beta ? scale_add(t[r], *p, beta) : t[r];
             TQ_ST(p, stored(v));
-            if constexpr (TRK) track(v);
+            track(v);
           });
         }
       }
@@ -665,9 +667,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     // S2Desc::epi: the last gate is applied here, in registers -- a thread reads the K inputs of
     // a group (slots r0 .. r0+K-1 of the pre-gate tile) and stores its N outputs (slots r0 ..
     // r0+N-1); the coefficients are wave-uniform (scalar registers)
-    auto store_epi = [&](auto kt, auto nt, auto tracked) {
+    auto store_epi = [&](auto kt, auto nt) {
       constexpr int K = decltype(kt)::value, N = decltype(nt)::value;
-      constexpr bool TRK = decltype(tracked)::value;
       // the coefficient row's offset is re-materialised per chunk: hoisted out of the chunk loop,
       // the per-case LDS addresses of every (K, N) instantiation were spilled to scratch and
       // reloaded one dependent round trip per read
@@ -690,16 +691,16 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
             T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + n]), sto);
             const T v = use_beta ? scale_add(acc, *p, beta) : acc;
             TQ_ST(p, stored(v));
-            if constexpr (TRK) track(v);
+            track(v);
           }
         }
         asm volatile("" ::: "memory");
       }
     };
-    auto store_epi_kn = [&](auto tracked) {
+    auto store_epi_kn = [&]() {
       using std::integral_constant;
 #define TQ_EPI(k, n) \
-  case k * 16 + n: store_epi(integral_constant<int, k>{}, integral_constant<int, n>{}, tracked); break;
+  case k * 16 + n: store_epi(integral_constant<int, k>{}, integral_constant<int, n>{}); break;
       const int32_t* gm = gmeta + (epi - 1) * kGm;
       switch (gm[kGmK] * 16 + gm[kGmN]) {
         TQ_EPI(1, 2) TQ_EPI(1, 4) TQ_EPI(1, 8) TQ_EPI(2, 2) TQ_EPI(2, 4) TQ_EPI(2, 8) TQ_EPI(4, 4)
@@ -707,11 +708,8 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       }
 #undef TQ_EPI
     };
-    if (epi) {
-      if (kC64 && amax) store_epi_kn(std::true_type{});
-      else store_epi_kn(std::false_type{});
-    } else if (kC64 && amax) store_chunk(std::true_type{});
-    else store_chunk(std::false_type{});
+    if (epi) store_epi_kn();
+    else store_chunk();
     __syncthreads();  // every wave has read the tile
     if (ch == lb) TQ_TS(5);
     if (more) fill(i + 1, nxt);
