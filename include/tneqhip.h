@@ -140,8 +140,11 @@ int tq_plan_create(tq_plan* plan, int dtype, int n_inputs, const int32_t* in_ran
  * TQ_LANE_ARENA_MB), "n_presplit" (pre-split GEMM candidates), "presplit_fallbacks" (slices
  * re-run on the split path so far).  -1 if unknown. */
 int64_t tq_plan_query(tq_plan plan, const char* key);
-/* Plan option: "graph" = 1 (default) replays the execute's launches from a captured hipGraph,
- * 0 launches them eagerly on the stream (use when the caller captures the stream itself). */
+/* Plan options: "graph" = 1 (default) replays the execute's launches from a captured hipGraph,
+ * 0 launches them eagerly on the stream (use when the caller captures the stream itself);
+ * "sweep_chain" = 1 (default, env TQ_S2_SEQ) runs consecutive hoisted levels that are each one
+ * small sweep2 op as one launch of one workgroup (query "n_chain_launches"), 0 one launch per
+ * level. */
 int tq_plan_set(tq_plan plan, const char* key, int64_t value);
 /* human-readable per-step description into buf (for debugging / DESIGN evidence) */
 int tq_plan_describe(tq_plan plan, char* buf, size_t n);

@@ -201,6 +201,10 @@ int tq_plan_set(tq_plan p, const char* key, int64_t value) {
     p->plan.use_graph = value != 0;
     return TQ_OK;
   }
+  if (k == "sweep_chain") {      // 0: the small sweep2 ops of a chain run one launch per level
+    p->plan.use_seq = value != 0;
+    return TQ_OK;
+  }
   tq::set_error("tq_plan_set: unknown key " + k);
   return TQ_ERR_INVALID;
 }
@@ -231,7 +235,12 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "n_sweep") return P.n_sweep;
   if (k == "n_sweep_gates") return P.n_sweep_gates;
   if (k == "n_sweep2") { int64_t c = 0; for (auto& o : P.ops) c += o.kind == tq::OP_SWEEP2; return c; }
-  if (k == "n_launch_once") return P.n_launch_once;
+  if (k == "n_launch_once") {   // launches of the hoisted part as executed (chain launches merged)
+    int64_t c = P.n_launch_once;
+    if (P.use_seq) for (auto& r : P.seq_once) c -= r.second - r.first - 1;
+    return c;
+  }
+  if (k == "n_chain_launches") return P.use_seq ? (int64_t)P.seq_once.size() : 0;
   if (k == "n_launch_slice") return P.n_launch_slice;
   if (k == "out_numel") return P.out_numel;
   return -1;

@@ -341,6 +341,15 @@ class Compiler {
         for (int j : g) d << " " << j;
         d << "\n";
       }
+    for (auto& r : P_.seq_once) {
+      d << "# chain launch (a workgroup per stream, one-chunk layouts): once entries " << r.first << ".."
+        << r.second - 1 << ", ops";
+      for (int i = r.first; i < r.second; ++i)
+        for (int j : P_.sched_once[i])
+          d << " " << j << "/s" << P_.seq_stream[j] << ((P_.ops[j].lds_io & 1) ? "<" : "")
+            << ((P_.ops[j].lds_io & 2) ? ">" : "");
+      d << "   (< input from LDS, > result left in LDS)\n";
+    }
     P_.describe = d.str();
     return TQ_OK;
   }
@@ -507,6 +516,148 @@ class Compiler {
     }
     P_.n_launch_once = (int)P_.sched_once.size();
     P_.n_launch_slice = (int)P_.sched_slice.size();
+    // chain launches: consecutive hoisted levels that are each one small sweep2 op (C2's whole
+    // contraction, the first levels of C3 / C4's hoisted chains: 1-4 workgroups per launch) run
+    // in order by one workgroup in one launch
+    // Levels of several such ops (the left and right halves of a cut network) run as several
+    // streams of one launch, a workgroup each, when every op conflicts (RAW / WAR / WAW) with
+    // earlier ops of at most one stream: that stream's workgroup runs it after them.
+    P_.seq_once.clear();
+    P_.seq_stream.assign(n, -1);
+    P_.use_seq = s2_seq_enabled();
+    auto chainable = [&](const std::vector<int>& g) {
+      if (g.empty() || (int)g.size() > kS2SeqMaxStreams) return false;
+      for (int j : g) {
+        const Op& op = P_.ops[j];
+        if (op.kind != OP_SWEEP2 || op.s2_dense || op.stab1 < 0) return false;
+      }
+      return true;
+    };
+    auto conflict = [&](int i, int j) {
+      return overlap(wr[i], rd[j]) || overlap(wr[i], wr[j]) || overlap(rd[i], wr[j]);
+    };
+    const int ns = (int)P_.sched_once.size();
+    for (int i = 0; i < ns;) {
+      if (!chainable(P_.sched_once[i])) { ++i; continue; }
+      std::vector<int> in_run;   // ops of the run so far
+      int nstreams = 0, nops = 0, e = i;
+      for (; e < ns && chainable(P_.sched_once[e]); ++e) {
+        const auto& g = P_.sched_once[e];
+        if (nops + (int)g.size() > kS2MaxOps) break;
+        std::vector<int> st(g.size(), -1);
+        int fresh = nstreams;
+        bool ok = true;
+        for (size_t q = 0; q < g.size() && ok; ++q) {
+          int s = -1;
+          for (int k : in_run)
+            if (conflict(k, g[q])) {
+              if (s >= 0 && P_.seq_stream[k] != s) { ok = false; break; }
+              s = P_.seq_stream[k];
+            }
+          st[q] = s >= 0 ? s : fresh++;
+        }
+        if (!ok || fresh > kS2SeqMaxStreams) break;
+        for (size_t q = 0; q < g.size(); ++q) { P_.seq_stream[g[q]] = st[q]; in_run.push_back(g[q]); }
+        nstreams = fresh;
+        nops += (int)g.size();
+      }
+      if (e - i >= 2) {
+        P_.seq_once.push_back({i, e});
+      } else {
+        for (int k : in_run) P_.seq_stream[k] = -1;
+        e = std::max(e, i + 1);
+      }
+      i = e;
+    }
+    // LDS hand-offs inside a chain launch: op j's result stays in the workgroup's LDS for the
+    // next op k of its stream when k reads exactly that tensor, it fits 64 KiB, and no other op
+    // reads it before it is overwritten (true reads: a, b, gate tensors; the scan follows the
+    // execution order: the rest of the hoisted launches, then every per-slice launch)
+    for (auto& o : P_.ops) o.lds_io = 0;
+    std::vector<int> order;   // execution order of the ops (hoisted, then per slice)
+    for (auto& g : P_.sched_once) for (int j : g) order.push_back(j);
+    for (auto& g : P_.sched_slice) for (int j : g) order.push_back(j);
+    std::vector<int> at(n, -1);
+    for (size_t q = 0; q < order.size(); ++q) at[order[q]] = (int)q;
+    auto true_reads = [&](int i) {
+      std::vector<Acc> v;
+      const Op& op = P_.ops[i];
+      add(v, op.a, op.na);
+      add(v, op.b, op.nb);
+      for (auto& g : op.sgates) add(v, g.g, g.n);
+      return v;
+    };
+    for (auto& r : P_.seq_once) {
+      std::vector<int> run;
+      for (int i = r.first; i < r.second; ++i) for (int j : P_.sched_once[i]) run.push_back(j);
+      // bit 2: no op of the launch writes this op's gate tensors (prefetch while the previous
+      // op of its stream runs)
+      for (int k : run) {
+        std::vector<Acc> gr;
+        for (auto& g : P_.ops[k].sgates) add(gr, g.g, g.n);
+        bool clean = true;
+        for (int i : run) clean = clean && !overlap(wr[i], gr);
+        if (clean && s2_seq_prefetch()) P_.ops[k].lds_io |= 4;
+      }
+      for (size_t x = 0; x < run.size(); ++x) {
+        const int j = run[x];
+        int k = -1;
+        for (size_t y = x + 1; y < run.size() && k < 0; ++y)
+          if (P_.seq_stream[run[y]] == P_.seq_stream[j]) k = run[y];
+        if (k < 0) continue;
+        const Op& oj = P_.ops[j];
+        const Op& ok = P_.ops[k];
+        if (oj.writes_output || oj.amax_word >= 0 || oj.ps_gemm >= 0 || oj.c.kind != ok.a.kind ||
+            oj.c.off != ok.a.off || oj.c.index != ok.a.index || oj.c.region != ok.a.region || oj.nc != ok.na || oj.nc * esz > kS2ChunkBytes)
+          continue;
+        std::vector<Acc> out;
+        add(out, oj.c, oj.nc);
+        if (out.size() != 1) continue;
+        bool alone = true;
+        for (size_t q = (size_t)at[j] + 1; q < order.size() && alone; ++q) {
+          const int i = order[q];
+          if (i == k) continue;
+          if (overlap(true_reads(i), out)) { alone = false; break; }
+          std::vector<Acc> w;
+          add(w, P_.ops[i].c, P_.ops[i].nc);
+          add(w, P_.ops[i].ws, P_.ops[i].nws);
+          bool covered = false;
+          for (auto& a : w) covered = covered || (a.space == out[0].space && a.lo <= out[0].lo && a.hi >= out[0].hi);
+          if (covered) break;   // overwritten: no later op reads j's values
+        }
+        if (!alone) continue;
+        P_.ops[j].lds_io |= 2;
+        P_.ops[k].lds_io |= 1;
+      }
+    }
+  }
+  // chain launches take small ops of at most this many chunks, in their one-chunk layout
+  // (TQ_S2_SEQCH, default 2).  Measured r04: C2's 29 levels of 4-chunk ops as one chain are
+  // 0.404 ms against 0.363 one launch per level on a fast box -- ~6 us of gate passes per op on
+  // ONE CU cost more than the ~3 us launch gap they save -- though 0.596 against 0.677 on a box
+  // with slow memory round trips; C3's 2-chunk levels: 0.677 against 0.684 ms
+  static int s2_seq_max_chunks() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_SEQCH");
+      return e ? atoi(e) : 2;
+    }();
+    return v;
+  }
+  // chain launches: the next op's descriptor prefetched (TQ_S2_SEQPF, default 1)
+  static bool s2_seq_prefetch() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_SEQPF");
+      return !(e && e[0] == '0');
+    }();
+    return v;
+  }
+  // chain launches on (TQ_S2_SEQ, default 1; tq_plan_set "sweep_chain" per plan)
+  static bool s2_seq_enabled() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_SEQ");
+      return !(e && e[0] == '0');
+    }();
+    return v;
   }
 
  private:
@@ -1198,6 +1349,7 @@ class Compiler {
       while ((2 << lg) <= mc) ++lg;
       lc = std::min(lc, std::max(std::min(s2_min_logc(), d.colbits), d.colbits - lg));
     }
+    if (one_chunk_) lc = std::min(lc_cap, d.colbits);   // the chain-launch form (Op::stab1)
     d.logC = lc;
     d.nchunks = int64_t(1) << (d.colbits - lc);
     // load / store enumerations: chunk bits by increasing memory stride
@@ -1491,7 +1643,7 @@ class Compiler {
 
   // one OP_SWEEP2 op: chain c (shape sh, layout d) from src (n0 elements) into tgt (nq)
   void emit_s2(const Chain& c, const ChainShape& sh, const S2Desc& d, BufRef src, int64_t n0, BufRef tgt,
-               int64_t nq, bool direct, const char* what) {
+               int64_t nq, bool direct, const char* what, const S2Desc* d1 = nullptr) {
     Op op;
     op.kind = OP_SWEEP2;
     op.a = src;
@@ -1518,6 +1670,14 @@ class Compiler {
     std::memcpy(blob.data(), &d, sizeof(S2Desc));
     op.stab = (int)P_.stabs.size();
     P_.stabs.push_back(std::move(blob));
+    if (d.nchunks == 1) {
+      op.stab1 = op.stab;
+    } else if (d1) {
+      std::vector<char> b1(sizeof(S2Desc));
+      std::memcpy(b1.data(), d1, sizeof(S2Desc));
+      op.stab1 = (int)P_.stabs.size();
+      P_.stabs.push_back(std::move(b1));
+    }
     op.flops = flops;
     op.bytes = (double)(n0 + nq) * P_.esz;
     std::ostringstream o;
@@ -1619,7 +1779,17 @@ class Compiler {
       } else {
         S2Desc d;
         if (!s2_layout(c, sh0, c.out_modes, &d)) { set_error("internal: sweep2 layout"); return TQ_ERR_INVALID; }
-        emit_s2(c, sh0, d, c.X0.buf, n0, tgt, nq, direct, "");
+        // a small tensor split into chunks for parallelism: also its one-chunk form, which a
+        // chain launch (one workgroup running consecutive dependent ops) uses
+        S2Desc d1;
+        bool has1 = false;
+        if (d.nchunks > 1 && d.nchunks <= s2_seq_max_chunks() &&
+            (d.ncols * (int64_t)sh0.tout_n) <= (int64_t(1) << s2_chunk_bits((int)P_.esz))) {
+          one_chunk_ = true;
+          has1 = s2_layout(c, sh0, c.out_modes, &d1) && d1.nchunks == 1;
+          one_chunk_ = false;
+        }
+        emit_s2(c, sh0, d, c.X0.buf, n0, tgt, nq, direct, "", has1 ? &d1 : nullptr);
       }
       res.modes = c.out_modes;
       for (int m : c.out_modes) res.ext.push_back(ext_[m]);
@@ -1996,6 +2166,7 @@ class Compiler {
 
   Plan& P_;
   int lanes_hint_ = 1;
+  bool one_chunk_ = false;   // s2_layout: one chunk of the whole tensor when it fits the tile
   bool cplx_ = false;
   int n_inputs_ = 0;
   Chain chain_;
@@ -2198,6 +2369,7 @@ int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, 
   key.inputs.assign(inputs, inputs + P.n_inputs);
   key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
   key.mode = P.run_mode;
+  key.seq = P.use_seq;
   constexpr size_t kMaxGraphs = 8;
   Plan::GraphEntry* hit = nullptr;
   for (auto& g : P.graphs) if (g.key == key) hit = &g;
@@ -2408,6 +2580,60 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       }
       return TQ_OK;
     };
+    // a sweep2 op's launch record from descriptor stabs[stab] (the current lane's pointers)
+    auto fill_s2 = [&](S2Op& o, const Op& op, int stab) -> int {
+      o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[stab]);
+      o.X = ptr(op.a);
+      o.Y = ptr(op.c);
+      const S2Desc* hd = reinterpret_cast<const S2Desc*>(P.stabs[stab].data());
+      for (size_t g = 0; g < op.sgates.size(); ++g) {
+        o.G[g] = ptr(op.sgates[g].g);
+        int mx = 0;
+        for (int t = 0; t < hd->gate[g].K * hd->gate[g].N; ++t) mx = std::max(mx, hd->gate[g].gidx[t] + 1);
+        if (mx > kS2GateRaw) { set_error("internal: sweep2 gate tensor too large"); return TQ_ERR_INVALID; }
+        o.gnum[g] = (uint8_t)mx;
+      }
+      o.beta = op.writes_output ? beta_out : 0.0;
+      o.use_beta = o.beta != 0.0;
+      o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
+      o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
+      return TQ_OK;
+    };
+    // Plan::seq_once run [b, e): its ops in order, one workgroup, one launch
+    auto launch_chain = [&](int b, int e) -> int {
+      Plan::Ev ev{};
+      const bool prof = (P.profile >> (int)OP_SWEEP) & 1;
+      if (prof) {
+        if (P.ev_free.empty()) {
+          TQ_HIP(hipEventCreate(&ev.a));
+          TQ_HIP(hipEventCreate(&ev.b));
+        } else {
+          ev = P.ev_free.back();
+          P.ev_free.pop_back();
+        }
+        ev.kind = (int)OP_SWEEP; ev.flops = 0; ev.bytes = 0;
+        TQ_HIP(hipEventRecord(ev.a, stream));
+      }
+      S2Launch L;
+      L.seq = 1;
+      for (int i = b; i < e; ++i)
+        for (int j : P.sched_once[i]) {
+          const Op& op = P.ops[j];
+          S2Op& o = L.op[L.nops++];
+          TQ_TRY(fill_s2(o, op, op.stab1));
+          o.lds_io = op.lds_io;
+          o.block_begin = P.seq_stream[j];   // the stream's workgroup
+          o.nblocks = 1;
+          ev.flops += op.flops;
+          ev.bytes += op.bytes;
+        }
+      TQ_TRY(sweep2_launch(P.dtype, L, stream));
+      if (prof) {
+        TQ_HIP(hipEventRecord(ev.b, stream));
+        P.ev_used.push_back(ev);
+      }
+      return TQ_OK;
+    };
     // one entry of the schedule: a single op, or independent sweep2 ops in one launch
     auto launch = [&](const std::vector<int>& grp) -> int {
       const Op& op0 = P.ops[grp[0]];
@@ -2489,24 +2715,10 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           set_lane(items[i0 + q].first);
           const Op& op = P.ops[items[i0 + q].second];
           S2Op& o = L.op[q];
-          o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[op.stab]);
-          o.X = ptr(op.a);
-          o.Y = ptr(op.c);
-          const S2Desc* hd = reinterpret_cast<const S2Desc*>(P.stabs[op.stab].data());
-          for (size_t g = 0; g < op.sgates.size(); ++g) {
-            o.G[g] = ptr(op.sgates[g].g);
-            int mx = 0;
-            for (int t = 0; t < hd->gate[g].K * hd->gate[g].N; ++t) mx = std::max(mx, hd->gate[g].gidx[t] + 1);
-            if (mx > kS2GateRaw) { set_error("internal: sweep2 gate tensor too large"); return TQ_ERR_INVALID; }
-            o.gnum[g] = (uint8_t)mx;
-          }
+          TQ_TRY(fill_s2(o, op, op.stab));
           o.block_begin = blocks;
           o.nblocks = s2_blocks(op.s2_nchunks);
           blocks += o.nblocks;
-          o.beta = op.writes_output ? beta_out : 0.0;
-          o.use_beta = o.beta != 0.0;
-          o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
-          o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
         }
         TQ_TRY(sweep2_launch(P.dtype, L, stream));
         }
@@ -2522,7 +2734,17 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     };
     if (sl == s_begin) {
       if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
-      for (auto& grp : P.sched_once) TQ_TRY(launch(grp));
+      size_t run = 0;
+      for (int i = 0; i < (int)P.sched_once.size();) {
+        while (P.use_seq && run < P.seq_once.size() && P.seq_once[run].first < i) ++run;
+        if (P.use_seq && run < P.seq_once.size() && P.seq_once[run].first == i) {
+          TQ_TRY(launch_chain(i, P.seq_once[run].second));
+          i = P.seq_once[run].second;
+          continue;
+        }
+        TQ_TRY(launch(P.sched_once[i]));
+        ++i;
+      }
     }
     // per-slice max words: one set per lane (pre-split mode: one set shared by the batch's
     // lanes, max-ed over all of them -- an upper bound of every lane's operand)

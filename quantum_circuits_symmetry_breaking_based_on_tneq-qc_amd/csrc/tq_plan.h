@@ -64,6 +64,13 @@ struct Op {
   int load_colfast = 1, store_colfast = 1;
   // sweep2: descriptor blob = stabs[stab] (an S2Desc), launched with s2_blocks(s2_nchunks)
   int64_t s2_nchunks = 0;
+  // sweep2 whose whole tensor fits one LDS tile: the one-chunk layout of the same chain
+  // (stabs[stab1]; == stab when the default layout is one chunk already, -1: none), the form a
+  // chain launch (Plan::seq_once) runs
+  int stab1 = -1;
+  // chain launches: bit 0 = X comes from the workgroup's LDS (the previous op of its stream left
+  // it there), bit 1 = Y stays in LDS for the next op of its stream (S2Op::lds_io)
+  int lds_io = 0;
   // dense sweep (tq_sweepd.hip): stabs[stab] is an S2Dense, b = the tout x tin coefficient
   // matrix written by the preceding compose op (a sweep2 op of the same chain on the identity)
   bool s2_dense = false;
@@ -159,6 +166,12 @@ struct Plan {
   // a launch.  `once` = slice-invariant ops (first slice of an execute call), `slice` = per slice
   std::vector<std::vector<int>> sched_once, sched_slice;
   int n_launch_once = 0, n_launch_slice = 0;
+  // chain launches: runs [first, last) of consecutive sched_once entries that are each ONE small
+  // sweep2 op (a one-chunk layout exists), run in order by one workgroup in one launch
+  // (S2Launch::seq) when use_seq (env TQ_S2_SEQ, default 1; tq_plan_set "sweep_chain")
+  std::vector<std::pair<int, int>> seq_once;
+  std::vector<int> seq_stream;   // per op: its stream (workgroup) in a chain launch, -1 none
+  bool use_seq = true;
   std::string describe;
   // hipGraph of the whole launch sequence of one execute call, replayed while the call's
   // pointers / slice range / flags are unchanged (a plan is hundreds of small launches)
@@ -168,9 +181,10 @@ struct Plan {
     int64_t b = 0, e = 0, s = 0;
     int acc = 0;
     int mode = 0;   // Plan::run_mode the graph was captured with
+    bool seq = true;  // Plan::use_seq
     bool operator==(const GraphKey& o) const {
       return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc &&
-             mode == o.mode;
+             mode == o.mode && seq == o.seq;
     }
   };
   bool use_graph = true;

@@ -118,7 +118,12 @@ struct S2Op {
   uint8_t gnum[kS2MaxGates] = {};
   int block_begin = 0, nblocks = 0;
   double beta = 0.0;
-  int use_beta = 0, pad = 0;
+  // lds_io (chain launches only, one-chunk ops of <= kS2ChunkBytes): bit 0 = X is in the launch's
+  // dynamic LDS block (left there by the previous op of this stream), bit 1 = Y goes there
+  // instead of memory (the next op of this stream is its only reader; no beta, no split, no max),
+  // bit 2 = no op of the launch writes this op's gate tensors (its descriptor and gate elements
+  // may be loaded while the previous op of its stream runs)
+  int use_beta = 0, lds_io = 0;
   // complex64 only, optional: the op atomically max-es the float bits of max |re|, |im| over
   // every value it stores into *amax (zeroed before; the max a consuming f16-split GEMM scales by)
   uint32_t* amax = nullptr;
@@ -128,8 +133,14 @@ struct S2Op {
   const int32_t* split_sc = nullptr;
 };
 
+// streams of a chain launch (S2Launch::seq), a workgroup each
+constexpr int kS2SeqMaxStreams = 8;
 struct S2Launch {
-  int nops = 0, pad = 0;
+  // seq = 0: independent ops (one dependency level), blockIdx ranges select the op; seq = 1:
+  // dependent chains -- workgroup b runs, in order, the ops whose block_begin is b (nblocks 1
+  // each; an op reads only what earlier ops of its own stream wrote): no launch gap between
+  // the small ops of a long chain, and the kernel's code stays in one CU's instruction cache
+  int nops = 0, seq = 0;
   S2Op op[kS2MaxOps];
 };
 

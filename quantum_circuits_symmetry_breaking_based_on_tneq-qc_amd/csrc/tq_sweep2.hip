@@ -369,8 +369,11 @@ __device__ __forceinline__ void run_gate(T* buf, const T* cf, const int32_t* gm,
 #undef TQ_GATE
 }
 
-template <typename T, int CB>
-__global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
+// SEQ: the chain-launch form (S2Launch::seq): one workgroup per CU (its streams are a few
+// workgroups; the LDS hand-off block takes 64 KiB more), so up to 256 VGPRs -- the op loop around
+// the body does not fit the 128 of the two-per-CU form without spilling
+template <typename T, int CB, bool SEQ>
+__global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   constexpr int RMAX = (1 << CB) / NT;
   // register copies of elements as plain vector words (16-byte struct arrays behind runtime
   // conditions are otherwise demoted to scratch)
@@ -382,15 +385,47 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   __shared__ T cf[kS2MaxGates * kCf];                    // gate coefficients, k*N+n
   static_assert(sizeof(S2Keep) % 8 == 0, "kept-table copy granularity");
   __shared__ uint2 keep_raw[sizeof(S2Keep) / 8];          // S2Desc::k, staged once
+  // chain launches (S2Launch::seq) with LDS hand-offs: the dynamic LDS holds the tensor an op
+  // passes to the next op of its stream, in its memory layout (S2Op::lds_io; <= 64 KiB)
+  extern __shared__ uint2 s2_dyn[];
+  Raw* const mir = reinterpret_cast<Raw*>(s2_dyn);
   const S2Keep& keep = *reinterpret_cast<const S2Keep*>(keep_raw);
   const int32_t* const gmeta = &keep.gmeta[0][0];        // K, N, pass mask, kaddr, naddr
   const int32_t* const pmeta = &keep.pmeta[0][0];        // passes
   const int32_t* const lut = &keep.lut[0][0];            // group -> LDS byte offset part
   const int tid = threadIdx.x;
-  // ---- which op this workgroup works on (wave-uniform scan over <= 16 ranges)
+  // ---- which op this workgroup works on: one op of a level (blockIdx ranges select it,
+  // wave-uniform scan), or -- S2Launch::seq, one workgroup -- every op of a dependent chain in
+  // order: op j + 1 reads what op j stored (same CU: its stores are complete before the next
+  // op's loads, below), and from the second op on the code is in this CU's instruction cache
   int j = 0;
   for (int q = 1; q < L.nops; ++q)
     if ((int)blockIdx.x >= L.op[q].block_begin) j = q;
+  const int j_end = SEQ ? L.nops : j + 1;
+  if (SEQ) j = 0;
+  // descriptor words / gate-tensor elements per thread of the coalesced staging copy
+  constexpr int kIt = (kDescWords2 + NT - 1) / NT, kGt = (kS2MaxGates * kS2GateRaw + NT - 1) / NT;
+  auto load_desc = [&](const S2Op& o, uint2 (&w)[kIt], Raw (&g)[kGt]) {
+    const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(o.desc);
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + it * NT;
+      if (i < kDescWords2) w[it] = gd[i];
+    }
+#pragma unroll
+    for (int it = 0; it < kGt; ++it) {
+      const int i = tid + it * NT;
+      const int gi = i / kS2GateRaw, e = i % kS2GateRaw;
+      if (i < kS2MaxGates * kS2GateRaw && e < (int)o.gnum[gi]) g[it] = reinterpret_cast<const Raw*>(o.G[gi])[e];
+    }
+  };
+  // SEQ: the next op of this stream's descriptor and gate elements, loaded into registers while
+  // this op runs (S2Op::lds_io bit 2: no earlier op of the launch writes its gate tensors)
+  uint2 pdw[kIt];
+  Raw pgw[kGt];
+  bool have_pf = false;
+  for (; j < j_end; ++j) {
+  if (SEQ && L.op[j].block_begin != (int)blockIdx.x) continue;   // another stream's op
   const S2Op& op = L.op[j];
   const S2Desc* __restrict__ d = op.desc;
 #ifdef TQ_S2_TIMING
@@ -412,24 +447,19 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   static_assert(kGrawOff + kS2MaxGates * kS2GateRaw <= (1 << CB), "descriptor + raw gates fit the tile");
   T* graw = buf + kGrawOff;
   {
-    const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(d);
     uint2* bd = reinterpret_cast<uint2*>(buf);
     uint2* kd = keep_raw;
     // every load is issued before the first LDS store (one memory round trip, not one per
     // loop iteration)
-    constexpr int kIt = (kDescWords2 + NT - 1) / NT, kGt = (kS2MaxGates * kS2GateRaw + NT - 1) / NT;
     uint2 dw[kIt];
     Raw gw[kGt];
+    if (SEQ && have_pf) {
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int i = tid + it * NT;
-      if (i < kDescWords2) dw[it] = gd[i];
-    }
+      for (int it = 0; it < kIt; ++it) dw[it] = pdw[it];
 #pragma unroll
-    for (int it = 0; it < kGt; ++it) {
-      const int i = tid + it * NT;
-      const int g = i / kS2GateRaw, e = i % kS2GateRaw;
-      if (i < kS2MaxGates * kS2GateRaw && e < (int)op.gnum[g]) gw[it] = reinterpret_cast<const Raw*>(op.G[g])[e];
+      for (int it = 0; it < kGt; ++it) gw[it] = pgw[it];
+    } else {
+      load_desc(op, dw, gw);
     }
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
@@ -455,6 +485,7 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   const int rin = (nin + NT - 1) / NT, rout = (nout + NT - 1) / NT;  // slots in use (powers of 2)
   const bool use_beta = op.use_beta;
   const double beta = op.beta;
+  const bool x_lds = SEQ && (op.lds_io & 1) != 0, y_lds = SEQ && (op.lds_io & 2) != 0;   // chain hand-offs
   // producer-side max of a complex64 GEMM operand (S2Op::amax): max |re|, |im| of the values
   // this thread stores, one atomic per wave after the chunk loop
   constexpr bool kC64 = std::is_same<T, c64>::value;
@@ -472,8 +503,17 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
     }
     return v;
   };
+  // a chain's previous op: its stores were issued before this op's descriptor loads and are
+  // complete (in L2, visible to this CU) before any wave loads this op's input
+  if (SEQ) __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   TQ_TS(1);
+  if constexpr (SEQ) {
+    int jn = j + 1;
+    while (jn < L.nops && L.op[jn].block_begin != (int)blockIdx.x) ++jn;
+    have_pf = jn < L.nops && (L.op[jn].lds_io & 4) != 0;
+    if (have_pf) load_desc(L.op[jn], pdw, pgw);
+  }
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
   const int ngates = ds->ngates;
   const int epi = ds->epi;   // S2Desc::epi (read before the tile overwrites the descriptor copy)
@@ -574,7 +614,12 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
   int64_t ch = lb;
   if (ch < nchunks) {
     const int64_t base = lane_bases ? lane64(cb_in, 0) : chunk_base(ch, keep.w_in);
-    TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
+    if (x_lds) {   // the previous op of this stream left the tensor in LDS (one chunk)
+      const int lm = (int)ldm;
+      TQ_BY_COUNT(RMAX, rin, reg0[r] = mir[(int)(base + keep.ld_hm[r]) + lm]);
+    } else {
+      TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
+    }
   }
   TQ_TS(41);   // first chunk's loads issued
   // ---- gate coefficients -> LDS
@@ -640,7 +685,10 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
           T t[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) t[q] = buf[sta ^ keep.st_ha[r0 + q]];
-          if (st_lane) {
+          if (st_lane && y_lds) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) reinterpret_cast<T*>(mir)[(int)(base + keep.st_hm[r0 + q]) + (int)stm] = t[q];
+          } else if (st_lane) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + q]), sto);
@@ -654,7 +702,9 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
       } else {
         T t[4];
         TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ keep.st_ha[r]]);
-        if (st_lane) {
+        if (st_lane && y_lds) {
+          TQ_BY_COUNT(4, rout, reinterpret_cast<T*>(mir)[(int)(base + keep.st_hm[r]) + (int)stm] = t[r]);
+        } else if (st_lane) {
           TQ_BY_COUNT(4, rout, {
             T* p = lane_at(Y + uniform(base + keep.st_hm[r]), sto);
             const T v = use_beta ? scale_add(t[r], *p, beta) : t[r];
@@ -688,6 +738,10 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
             T acc = mul(x[0], c[n]);
 #pragma unroll
             for (int k = 1; k < K; ++k) mac(acc, x[k], c[k * N + n]);
+            if (y_lds) {
+              reinterpret_cast<T*>(mir)[(int)(base + keep.st_hm[r0 + n]) + (int)stm] = acc;
+              continue;
+            }
             T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + n]), sto);
             const T v = use_beta ? scale_add(acc, *p, beta) : acc;
             TQ_ST(p, stored(v));
@@ -728,11 +782,39 @@ __global__ void __launch_bounds__(NT, 4) sweep2_kernel(S2Launch L) {
 #endif
 #undef TQ_BY_COUNT
 #undef TQ_SLOTS
+  }  // ops
 }
 
 template <typename T>
 int launch_t(const S2Launch& L, hipStream_t stream) {
   constexpr int CB = sizeof(T) > 8 ? 12 : 13;
+  if (L.seq) {   // dependent chains: workgroup b runs the ops of stream b in order
+    int streams = 0;
+    bool lds = false;
+    for (int q = 0; q < L.nops; ++q) {
+      if (L.op[q].block_begin < 0 || L.op[q].block_begin >= kS2SeqMaxStreams || L.op[q].nblocks != 1) {
+        set_error("sweep2: a chain launch runs one workgroup per stream");
+        return TQ_ERR_INVALID;
+      }
+      streams = std::max(streams, L.op[q].block_begin + 1);
+      lds = lds || L.op[q].lds_io != 0;
+    }
+    // LDS hand-offs: a 64-KiB dynamic block beside the kernel's ~76 KiB (one workgroup per CU)
+    const unsigned dyn = lds ? (unsigned)kS2ChunkBytes : 0u;
+    if (dyn) {
+      static DeviceCache<1> attr;
+      if (attr.get(0, [] {
+            return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep2_kernel<T, CB, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kS2ChunkBytes) == hipSuccess ? 1 : -1;
+          }) < 0) {
+        set_error("sweep2: dynamic LDS for chain hand-offs");
+        return TQ_ERR_INVALID;
+      }
+    }
+    hipLaunchKernelGGL((sweep2_kernel<T, CB, true>), dim3((unsigned)streams), dim3(NT), dyn, stream, L);
+    TQ_HIP(hipGetLastError());
+    return TQ_OK;
+  }
   int blocks = 0;
   for (int q = 0; q < L.nops; ++q) blocks = std::max(blocks, L.op[q].block_begin + L.op[q].nblocks);
   if (blocks <= 0) return TQ_OK;
@@ -754,7 +836,7 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&sweep2_kernel<T, CB>), NT, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&sweep2_kernel<T, CB, false>), NT, 0) != hipSuccess)
       return -1;
     return std::max(1, (int)(cus * std::max(1, per) * rounds));
   }));
@@ -766,11 +848,11 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
       R.op[q].block_begin = b;
       b += R.op[q].nblocks;
     }
-    hipLaunchKernelGGL((sweep2_kernel<T, CB>), dim3((unsigned)b), dim3(NT), 0, stream, R);
+    hipLaunchKernelGGL((sweep2_kernel<T, CB, false>), dim3((unsigned)b), dim3(NT), 0, stream, R);
     TQ_HIP(hipGetLastError());
     return TQ_OK;
   }
-  hipLaunchKernelGGL((sweep2_kernel<T, CB>), dim3((unsigned)blocks), dim3(NT), 0, stream, L);
+  hipLaunchKernelGGL((sweep2_kernel<T, CB, false>), dim3((unsigned)blocks), dim3(NT), 0, stream, L);
   TQ_HIP(hipGetLastError());
   return TQ_OK;
 }

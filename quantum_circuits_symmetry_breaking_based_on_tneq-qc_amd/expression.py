@@ -55,6 +55,11 @@ class NativePlan:
     def query(self, key: str) -> int:
         return int(_lib.lib().tq_plan_query(self._h, key.encode()))
 
+    def set(self, key: str, value: int) -> None:
+        """Plan option (tq_plan_set): "graph" (replay a captured hipGraph, default 1),
+        "sweep_chain" (chain launches of small dependent sweep2 ops, default 1)."""
+        check(_lib.lib().tq_plan_set(self._h, key.encode(), int(value)), "tq_plan_set")
+
     def describe(self) -> str:
         L = _lib.lib()
         n = L.tq_plan_describe(self._h, None, 0)

@@ -50,6 +50,30 @@ def test_c2_single_amplitude_vs_oracle(dev):
         assert abs(got - ref) / abs(ref) < tol
 
 
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_chain_launch_equals_one_launch_per_level(dev, cfg):
+    """Consecutive small hoisted sweep2 levels run as ONE chain launch by default (a workgroup
+    per stream, one-chunk layouts, LDS hand-offs between the ops of a stream: tq_plan.cpp
+    Plan::seq_once, S2Launch::seq) -- C3's and C4's first levels; the same plan with
+    "sweep_chain" = 0 launches them level by level (multi-chunk layouts).  The per-element
+    arithmetic is the same gate sequence, so the two agree to rounding; a replay is exact.
+    (C2's levels with TQ_S2_SEQCH=4 are the same mechanism on one stream.)"""
+    import torch
+    from tneq_qc_amd.circuits import config_task
+    t = config_task(cfg)
+    for dt, tol in ((torch.complex128, 1e-13), (torch.complex64, 1e-6)):
+        e, ops = _expr_and_ops(t, dev, dt)
+        p = e.plan(dt)
+        assert p.query("n_chain_launches") == 1
+        a = e(*ops).cpu().numpy()
+        p.set("sweep_chain", 0)
+        assert p.query("n_chain_launches") == 0
+        b = e(*ops).cpu().numpy()
+        p.set("sweep_chain", 1)
+        c = e(*ops).cpu().numpy()
+        assert np.abs(a - b).max() <= tol * np.abs(b).max() and np.array_equal(a, c)
+
+
 _ORACLE_SLICES = {}
 
 

@@ -137,7 +137,10 @@ def test_launch_schedule_covers_every_op_once_and_batches_sweeps():
     for g in once + per:
         if len(g) > 1:
             assert len(g) <= 32 and all("SWEEP2" in ops[j] for j in g)
-    assert p.query("n_launch_once") == len(once) and p.query("n_launch_slice") == len(per)
+    # chain launches merge runs of hoisted levels (each run: one launch)
+    chains = [l for l in d if l.startswith("# chain launch")]
+    merged = sum(int(l.split("..")[1].split(",")[0]) - int(l.split("entries ")[1].split("..")[0]) for l in chains)
+    assert p.query("n_launch_once") == len(once) - merged and p.query("n_launch_slice") == len(per)
     assert p.query("n_sweep2") > 60 and len(once) < p.query("n_ops_once")
     # the GEMM of a slice waits for both branch sweeps: it is alone in its launch, after them
     gi = [k for k, g in enumerate(per) for j in g if "GEMM" in ops[j]]
@@ -236,6 +239,27 @@ def test_slice_lanes_within_the_arena_budget():
     assert p4.query("lanes") == 4   # 1.1-GiB per-slice part: 4 lanes in the 6-GiB budget
     e2, p2 = _plan(config_task("C2"))
     assert p2.query("lanes") == 1   # one slice
+
+
+def test_small_hoisted_levels_run_as_one_chain_launch():
+    """Consecutive hoisted levels of small sweep2 ops (the whole tensor fits one 64-KiB tile and
+    the default layout has at most 2 chunks) run as one chain launch, a workgroup per stream
+    (tq_plan.cpp Plan::seq_once): the first levels of C2, C3 and C4 (C3 / C4: the left and right
+    halves on streams of their own); consecutive ops of a stream hand their tensor over in LDS.
+    C2's later 4-chunk levels stay one launch each (measured faster, tq_plan.cpp
+    s2_seq_max_chunks); "sweep_chain" = 0 restores one launch per level."""
+    for cfg in ("C2", "C3", "C4"):
+        e, p = _plan(config_task(cfg))
+        d = [l for l in p.describe().splitlines() if l.startswith("# chain launch")]
+        assert len(d) == 1 and "<" in d[0] and ">" in d[0], d
+        assert ("/s1" in d[0]) == (cfg != "C2")
+        n_on = p.query("n_launch_once")
+        ops = d[0].split("ops")[1].split("(")[0].split()
+        levels = int(d[0].split("..")[1].split(",")[0]) - int(d[0].split("entries ")[1].split("..")[0]) + 1
+        assert p.query("n_chain_launches") == 1 and levels >= 3 and len(ops) >= (3 if cfg == "C2" else 6)
+        p.set("sweep_chain", 0)
+        assert p.query("n_chain_launches") == 0 and p.query("n_launch_once") == n_on + levels - 1
+        p.set("sweep_chain", 1)
 
 
 @pytest.mark.parametrize("cfg", ["C3", "C4"])
