@@ -71,12 +71,12 @@ def setup(dev, ks=None):
         bw = BrickWall(N_Q, DEPTH, seed=100 + k, mask=[idx])
         expr, eq = split_merge_expression(bw.qctn)
         params = [torch.nn.Parameter(torch.from_numpy(bw.cores[c].copy()).to(dev)) for c in bw.qctn.cores]
-        opt = SGDG(params, lr=1e-2, stiefel=True, momentum=0.9)
-        # the candidate's own stream of the SGDG retraction draws (the global `random` the
-        # reference draws from is swapped in around its step): results independent of the rank
-        # layout
-        rstate = [random.Random(1000 + k).getstate()]
-        cands.append((expr, params, opt, bw, eq, rstate))
+        # the candidate's own stream of the SGDG retraction draws (the reference draws from the
+        # global `random`; SGDG's rng= gives each concurrently trained candidate its own):
+        # results independent of the rank layout
+        rng = random.Random(1000 + k)
+        opt = SGDG(params, lr=1e-2, stiefel=True, momentum=0.9, rng=rng)
+        cands.append((expr, params, opt, bw, eq, rng))
     return target, cands
 
 
@@ -100,6 +100,52 @@ def capture(target, cands, dev):
     return graphs
 
 
+def capture_all(target, cands, dev, warmup=2):
+    """Every candidate's forward + loss + backward in ONE hipGraph: candidate k on a stream of
+    its own inside the capture (fork / join), so the graph holds 8 independent branches."""
+    cap = torch.cuda.Stream(dev)
+    sts = [torch.cuda.Stream(dev) for _ in cands]
+
+    def run_all():
+        losses = []
+        cur = torch.cuda.current_stream(dev)
+        for (expr, params, _, _, _, _), st in zip(cands, sts):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                loss = fidelity_loss(expr(*params), target)
+                loss.backward()
+            losses.append(loss)
+        for st in sts:
+            cur.wait_stream(st)
+        return losses
+
+    allp = [p for c in cands for p in c[1]]
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cap):
+        for _ in range(warmup):
+            for p in allp:
+                p.grad = None
+            run_all()
+    torch.cuda.current_stream(dev).wait_stream(cap)
+    torch.cuda.synchronize(dev)
+    for p in allp:
+        p.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        losses = run_all()
+    torch.cuda.synchronize(dev)
+    return g, losses
+
+
+def gpu_step_one_graph(target, cands, graph_all):
+    """capture_all's graph replayed once, then every candidate's SGDG step."""
+    g, losses = graph_all
+    g.replay()
+    for (_, _, opt, _, _, _) in cands:
+        opt.step()
+    return losses
+
+
 def gpu_step(target, cands, streams=None, graphs=None):
     """One training step of every candidate.  With `streams`, candidate k runs on streams[k]: the
     candidates are independent fits, so their latency-bound launch chains (each plan replays its
@@ -107,7 +153,7 @@ def gpu_step(target, cands, streams=None, graphs=None):
     (capture()), forward + loss + backward of candidate k is one graph replay."""
     losses = []
     cur = torch.cuda.current_stream()
-    for k, (expr, params, opt, _, _, rstate) in enumerate(cands):
+    for k, (expr, params, opt, _, _, _) in enumerate(cands):
         st = streams[k] if streams else cur
         if streams:
             st.wait_stream(cur)
@@ -119,9 +165,7 @@ def gpu_step(target, cands, streams=None, graphs=None):
                 opt.zero_grad()
                 loss = fidelity_loss(expr(*params), target)
                 loss.backward()
-            random.setstate(rstate[0])
             opt.step()
-            rstate[0] = random.getstate()
         losses.append(loss)
     if streams:
         for st in streams:
@@ -222,6 +266,8 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="forward / loss / backward issued eagerly every step (default: one hipGraph per candidate)")
     ap.add_argument("--port", type=int, default=0, help="gloo timing group port (multi-rank)")
+    ap.add_argument("--one-graph", action="store_true",
+                    help="every candidate's forward + loss + backward in ONE hipGraph (branches on forked streams)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -237,16 +283,19 @@ def main():
     _log(f"rank {rank}: setting up {len(mine)} candidates")
     target, cands = setup(dev, set(mine))
     streams = None if a.one_stream else [torch.cuda.Stream(dev) for _ in cands]
-    graphs = None if a.eager else capture(target, cands, dev)
+    graph_all = capture_all(target, cands, dev) if a.one_graph else None
+    graphs = None if (a.eager or a.one_graph) else capture(target, cands, dev)
+    step = (lambda: gpu_step_one_graph(target, cands, graph_all)) if graph_all else \
+        (lambda: gpu_step(target, cands, streams, graphs))
     for _ in range(a.warmup):
-        gpu_step(target, cands, streams, graphs)
+        step()
     torch.cuda.synchronize()
     _log(f"rank {rank}: warmup done; timing {a.steps} steps")
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        losses = gpu_step(target, cands, streams, graphs)
+        losses = step()
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     dt_local = time.perf_counter() - t0
@@ -272,7 +321,7 @@ def main():
            "candidates_per_rank": [len(range(r, len(CANDIDATES), world)) for r in range(world)],
            "cores_per_candidate": len(cands[0][1]), "dtype": "c128",
            "streams": len(streams) if streams else 1,
-           "step_graphs": graphs is not None,
+           "step_graphs": "one graph, a branch per candidate" if graph_all else graphs is not None,
            "forward": "QCTN.split halves swept + boundary contraction (split/merge path), one native plan",
            "amplitudes_per_forward": int(np.prod(cands[0][0].out_shape)),
            "host_issue_ms_per_step": [float(t[2]) / a.steps * 1e3 for t in allt],

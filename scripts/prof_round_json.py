@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""Summarize scripts/prof_r03.sh: per kernel family (boundary GEMM, dense sweep, sweep2) and launch
+"""Summarize scripts/prof_round.sh <tag>: per kernel family (boundary GEMM, dense sweep, sweep2) and launch
 shape (grid size), the average counters per dispatch over the PMC passes, the trace duration, the
 HBM bytes (2*FETCH_SIZE + WRITE_SIZE, kB; the gfx950 FETCH correction of MI355X_MICROARCH.md), the
 effective shader clock (GRBM_GUI_ACTIVE / 8 XCDs / duration), the MFMA busy fraction and the
-wave-cycle shares.  Writes profiles/pmc_c4_r03.json, profiles/pmc_gemm_f16_r03.json (the schema
-bench.py reads for the roofline) and profiles/rocprof_r03_bench_kernel_stats.csv."""
+wave-cycle shares.  Writes profiles/pmc_c4_<tag>.json, profiles/pmc_gemm_f16_<tag>.json (the
+schema bench.py reads for the roofline) and profiles/rocprof_<tag>_bench_kernel_stats.csv.
+    python3 scripts/prof_round_json.py gpurun_out/p<tag> <tag>"""
 import collections, csv, json, os, shutil, sys
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/p03"
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/p04"
+TAG = sys.argv[2] if len(sys.argv) > 2 else "r04"
 FAM = {"gemm_f16_split": "split_kernel", "dense_sweep": "sweepd_kernel", "sweep2": "sweep2_kernel"}
 
 
@@ -42,7 +44,7 @@ def dispatches(path, value_col=True):
 trace = dispatches(f"{root}/k0/run_kernel_trace.csv", value_col=False)
 passes = [dispatches(f"{root}/p{i}/run_counter_collection.csv") for i in (1, 2, 3, 4)]
 res = {"config": "C4",
-       "command": "scripts/prof_r03.sh: rocprofv3 --pmc <set> --kernel-include-regex "
+       "command": f"scripts/prof_round.sh {TAG}: rocprofv3 --pmc <set> --kernel-include-regex "
                   "'split_kernel|sweepd_kernel|sweep2_kernel' -- python3 bench.py --no-cpu-baseline --no-c5 "
                   "--no-alt --steps 2 --warmup 1 (4 counter passes + a kernel-trace pass of the same command)",
        "definitions": {
@@ -77,7 +79,7 @@ for key in sorted(trace, key=lambda k: (k[0], -len(trace[k]))):
         g["hbm_GBps"] = hb / avg_ns
     res["groups"].append(g)
 os.makedirs("profiles", exist_ok=True)
-json.dump(res, open("profiles/pmc_c4_r03.json", "w"), indent=1)
+json.dump(res, open(f"profiles/pmc_c4_{TAG}.json", "w"), indent=1)
 
 # the boundary GEMM in the schema bench.py reads (pmc_gemm_f16_r0N.json)
 gg = [g for g in res["groups"] if g["family"] == "gemm_f16_split"]
@@ -110,10 +112,10 @@ if gg:
            "algorithmic_bytes_per_launch": batch * ((M * K + N * K) * 8 + M * N * 8),
            "definition": res["definitions"]["mfma_busy_frac"] + "; " + res["definitions"]["hbm_bytes"]
                          + "; algorithmic bytes = batch x (A + B once + C written)"}
-    json.dump(gem, open("profiles/pmc_gemm_f16_r03.json", "w"), indent=1)
+    json.dump(gem, open(f"profiles/pmc_gemm_f16_{TAG}.json", "w"), indent=1)
 st = f"{root}/kt/run_kernel_stats.csv"
 if os.path.exists(st):
-    shutil.copy(st, "profiles/rocprof_r03_bench_kernel_stats.csv")
+    shutil.copy(st, f"profiles/rocprof_{TAG}_bench_kernel_stats.csv")
 for g in res["groups"]:
     print(g["family"], g["grid"], g["dispatches"], f"{g['avg_ns']/1e3:.1f}us",
           {k: round(g[k], 3) for k in ("effective_clock_GHz", "mfma_busy_frac", "wait_frac", "wait_lds_frac")
