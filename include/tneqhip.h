@@ -31,6 +31,8 @@
  *                       _eval_hermitenorm_batch(_np) (tneq_qc/core/engine_siamese.py:59-254).
  *   tq_inverse_cdf_sample — the clamp / cumsum / normalise / search / interpolate block of
  *                       EngineSiamese.sample (tneq_qc/core/engine_siamese.py:854-905).
+ *   tq_fidelity_forward / _backward — the symmetry-breaking fit's fidelity loss
+ *                       (symmetry_breaking_quantum.py:220-229) and its gradient, one launch each.
  *   tq_sgdg_step       — SGDG.step, the Stiefel / Cayley optimizer of the symmetry-breaking
  *                       training loop (tneq_qc/optim/stiefel_optimizer_complex.py:77-176,
  *                       called at symmetry_breaking_quantum.py:216-230).
@@ -188,6 +190,21 @@ int tq_hermite_features(int dtype, int64_t n_points, int K, const double* x, con
 int tq_inverse_cdf_sample(int dtype, int64_t n_rows, int64_t grid_size, const void* density,
                           int64_t ld_density, const void* grid_x, const float* u, void* samples,
                           int64_t samples_stride, void* stream);
+
+/* Fidelity loss of the symmetry-breaking fit (symmetry_breaking_quantum.py:220-229, the loss of
+ * every pruning candidate; validate_target_tensor :159-166), over n complex elements (dtype
+ * TQ_C64 / TQ_C128, t = target, o = the contraction's output, both device):
+ *   a = <t, o> = sum conj(t_i) o_i, T = <t, t>, N = <o, o>, L = 1 - |a|^2 / max(T N, 1e-12)
+ * forward: stats (device, 4 float64) = Re a, Im a, T, N; loss (device, one real of the dtype's
+ * precision) = L; float64 accumulation, one workgroup.
+ * backward: grad_o (device, n complex) = g * 2 dL/d(conj o) (torch's gradient of a real loss
+ * w.r.t. a complex tensor), g = device pointer to the upstream gradient of L (one real):
+ *   grad_o_i = 2 g (-a t_i / D + |a|^2 T o_i / D^2), D = max(T N, 1e-12), the second term only
+ *   when T N >= 1e-12 (the clamp passes no gradient).                                        */
+int tq_fidelity_forward(int dtype, int64_t n, const void* t, const void* o, double* stats, void* loss,
+                        void* stream);
+int tq_fidelity_backward(int dtype, int64_t n, const void* t, const void* o, const double* stats,
+                         const void* g, void* grad_o, void* stream);
 
 /* One SGDG optimizer step (tneq_qc/optim/stiefel_optimizer_complex.py:77-176, SGDG.step, with
  * gutils.py unit / qr_retraction / matrix_norm_one) for n parameters of one group, one workgroup

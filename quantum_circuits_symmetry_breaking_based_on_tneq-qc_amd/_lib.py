@@ -24,7 +24,7 @@ EXPORTED = (
     "tq_gemm_workspace_size", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
     "tq_plan_create", "tq_plan_query", "tq_plan_set", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
     "tq_plan_profile", "tq_plan_profile_read", "tq_hermite_features", "tq_inverse_cdf_sample",
-    "tq_sgdg_step",
+    "tq_sgdg_step", "tq_fidelity_forward", "tq_fidelity_backward",
 )
 TQ_SGDG_STIEFEL, TQ_SGDG_BUF_INIT, TQ_SGDG_RETRACT = 1, 2, 4
 TQ_HERMITE_MAX_K, TQ_ICDF_MAX_GRID = 128, 8192
@@ -75,6 +75,8 @@ _SIGS = {
                                        _vp, _vp]),
     "tq_inverse_cdf_sample": (_c.c_int, [_c.c_int, _c.c_int64, _c.c_int64, _vp, _c.c_int64, _vp, _vp, _vp,
                                          _c.c_int64, _vp]),
+    "tq_fidelity_forward": (_c.c_int, [_c.c_int, _c.c_int64, _vp, _vp, _vp, _vp, _vp]),
+    "tq_fidelity_backward": (_c.c_int, [_c.c_int, _c.c_int64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tq_sgdg_step": (_c.c_int, [_c.c_int, _c.c_int, _c.POINTER(_vp), _c.POINTER(_vp), _c.POINTER(_vp),
                                 _i32p, _i32p, _i32p, _c.c_double, _c.c_double, _c.c_double,
                                 _c.c_double, _c.c_int, _vp]),

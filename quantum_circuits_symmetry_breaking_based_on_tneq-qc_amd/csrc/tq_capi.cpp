@@ -317,6 +317,24 @@ int tq_inverse_cdf_sample(int dtype, int64_t n_rows, int64_t grid_size, const vo
   TQ_GUARD_END
 }
 
+int tq_fidelity_forward(int dtype, int64_t n, const void* t, const void* o, double* stats, void* loss,
+                        void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(n >= 0, "n");
+  TQ_CHECK_ARG(t && o && stats && loss, "null pointer");
+  return tq::fidelity_forward_launch(dtype, n, t, o, stats, loss, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
+int tq_fidelity_backward(int dtype, int64_t n, const void* t, const void* o, const double* stats,
+                         const void* g, void* grad_o, void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(n >= 0, "n");
+  TQ_CHECK_ARG(t && o && stats && g && grad_o, "null pointer");
+  return tq::fidelity_backward_launch(dtype, n, t, o, stats, g, grad_o, (hipStream_t)stream);
+  TQ_GUARD_END
+}
+
 int tq_plan_destroy(tq_plan p) {
   if (!p) return TQ_OK;
   tq::plan_release(p->plan);

@@ -178,5 +178,10 @@ int hermite_launch(int dtype, int64_t n, int K, const double* x, const double* w
 int icdf_launch(int dtype, int64_t rows, int64_t grid_size, const void* density, int64_t ld,
                 const void* grid_x, const float* u, void* out, int64_t out_stride,
                 hipStream_t stream);
+// fidelity loss of the symmetry-breaking fit (tq_loss.hip)
+int fidelity_forward_launch(int dtype, int64_t n, const void* t, const void* o, double* stats, void* loss,
+                            hipStream_t stream);
+int fidelity_backward_launch(int dtype, int64_t n, const void* t, const void* o, const double* stats,
+                             const void* g, void* grad, hipStream_t stream);
 
 }  // namespace tq

@@ -47,6 +47,10 @@ static int env_int(const char* name, int dflt = 0) {
 // (loads two K-steps ahead), room made by the ordered term pairs (5.13 vs 5.19-5.25 ms).
 // Measurements: DESIGN.md §3
 static std::atomic<int> g_gemm_f16_var{env_int("TQ_GEMM_F16_VAR", 6)};
+// static wave priority in the f16 split kernel (TQ_GEMM_PRIO=1): the second-dispatched half of
+// the 8 waves (threads >= NT / 2) runs at s_setprio 1 for the whole main loop
+// (cdna_hip_programming.md T5 static form: the younger half loses VALU arbitration otherwise)
+static const int g_gemm_prio = env_int("TQ_GEMM_PRIO", 0);
 int gemm_f16_var() { return g_gemm_f16_var.load(std::memory_order_relaxed); }
 bool gemm_3m() { return g_gemm_3m.load(std::memory_order_relaxed) != 0; }
 // The complex64 K-outer fast path runs on the bf16 matrix cores with an exact 3-term split of
@@ -441,6 +445,7 @@ struct FastArgs {
   const int32_t* sc_b;
   uint32_t* bad;
   int amax_bs_a, amax_bs_b;  // max-word stride between batch entries (0: one word per operand)
+  int prio;                  // f16 split kernel: s_setprio 1 for the second half of the waves
 };
 
 template <int N>
@@ -1267,6 +1272,8 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   using I5 = std::integral_constant<int, 5>;
 
   static_assert(NSET >= 2 && NSET <= 4, "register sets");
+  // wave-uniform guard (readfirstlane): s_setprio ignores EXEC
+  if (g.prio && __builtin_amdgcn_readfirstlane(tid) >= TL::NT / 2) __builtin_amdgcn_s_setprio(1);
   if constexpr (TL::SLOTS == 4) {
     // 4-slot ring: K-step u is loaded 5 steps ahead into set u % 4, split at step u - 2 into
     // slot u % 4, read and multiplied at step u; a barrier after every odd step -- between any
@@ -2219,6 +2226,7 @@ int launch_typed(int transA, int transB, int64_t M, int64_t N, int64_t K, int64_
       const bool g3 = gemm_3m();
       f.kchunk = K / fs;
       f.splits = fs; f.batch = (int)batch; f.beta = (float)beta;
+      f.prio = g_gemm_prio;
       if (gemm_bf16()) {
         using TX = xbf::TileX;
         static_assert(TX::BM == xbf::TileH::BM && TX::BN == xbf::TileH::BN && TX::BM == xbf::TileH4::BM, "same split-K tiling");

@@ -194,3 +194,49 @@ def inverse_cdf_sample(density: torch.Tensor, grid: torch.Tensor, u: torch.Tenso
                                           ctypes.c_void_p(_stream_ptr(dev)))
     check(rc, "tq_inverse_cdf_sample")
     return out
+
+
+class _FidelityLoss(torch.autograd.Function):
+    """L = 1 - |<t, o>|^2 / max(<t, t> <o, o>, 1e-12) (symmetry_breaking_quantum.py:220-229):
+    one launch forward (tq_fidelity_forward), one backward (tq_fidelity_backward); the target
+    gets no gradient (it is a constant of the fit)."""
+
+    @staticmethod
+    def forward(ctx, out_f, tgt_f):
+        dev = _require_device(out_f, tgt_f)
+        o = out_f.contiguous()
+        t = tgt_f.contiguous()
+        stats = torch.empty(4, dtype=torch.float64, device=dev)
+        loss = torch.empty((), dtype=o.real.dtype, device=dev)
+        check(_lib.lib().tq_fidelity_forward(dtype_code(o.dtype), o.numel(), ctypes.c_void_p(t.data_ptr()),
+                                             ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(stats.data_ptr()),
+                                             ctypes.c_void_p(loss.data_ptr()), ctypes.c_void_p(_stream_ptr(dev))),
+              "tq_fidelity_forward")
+        ctx.save_for_backward(o, t, stats)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        o, t, stats = ctx.saved_tensors
+        dev = o.device
+        gg = g.to(dtype=o.real.dtype).contiguous()
+        grad = torch.empty_like(o)
+        check(_lib.lib().tq_fidelity_backward(dtype_code(o.dtype), o.numel(), ctypes.c_void_p(t.data_ptr()),
+                                              ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(stats.data_ptr()),
+                                              ctypes.c_void_p(gg.data_ptr()), ctypes.c_void_p(grad.data_ptr()),
+                                              ctypes.c_void_p(_stream_ptr(dev))), "tq_fidelity_backward")
+        return grad, None
+
+
+def fidelity_loss(out: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """The symmetry-breaking fit's loss 1 - |<target, out>|^2 / max(<target, target> <out, out>,
+    1e-12) over the flattened tensors (symmetry_breaking_quantum.py:220-229: vdot, abs()**2,
+    clamp_min, 1 - num/den), differentiable w.r.t. ``out``; complex64 / complex128 on the HIP
+    device.  Returns a 0-d real tensor."""
+    if out.dtype not in (torch.complex64, torch.complex128) or target.dtype != out.dtype:
+        raise ValueError(f"fidelity_loss: complex64 / complex128 operands of one dtype (got {out.dtype}, {target.dtype})")
+    if out.numel() != target.numel():
+        raise ValueError(f"fidelity_loss: {out.numel()} vs {target.numel()} elements")
+    if target.requires_grad:
+        raise ValueError("fidelity_loss: the target is a constant (no gradient)")
+    return _FidelityLoss.apply(out.reshape(-1), target.reshape(-1))

@@ -80,7 +80,17 @@ def setup(dev, ks=None):
     return target, cands
 
 
+# the GPU step's loss: the fused kernels (tneq_qc_amd.ops.fidelity_loss, one launch each way)
+# unless C5_TORCH_LOSS=1 (the reference's torch expression, ~25 launches)
+USE_FUSED_LOSS = os.environ.get("C5_TORCH_LOSS", "0") != "1"
+
+
 def fidelity_loss(out, tgt):
+    """symmetry_breaking_quantum.py:224-228; on the HIP device the fused op, on the host (the CPU
+    baseline and the parity checker) the reference's torch expression."""
+    if out.is_cuda and USE_FUSED_LOSS:
+        from tneq_qc_amd.ops import fidelity_loss as fused
+        return fused(out, tgt)
     out_f = out.reshape(-1)
     num = torch.vdot(tgt, out_f).abs() ** 2
     den = (torch.vdot(tgt, tgt).real * torch.vdot(out_f, out_f).real).clamp_min(1e-12)
