@@ -10,5 +10,5 @@ for r in 1 2; do
   c5 "C5_TORCH_LOSS=0" "" || exit 2
   c5 "C5_TORCH_LOSS=0" "--one-graph" || exit 2
 done
-scripts/ab_env.sh "p0:TQ_GEMM_PRIO=0" "p1:TQ_GEMM_PRIO=1" "p0b:TQ_GEMM_PRIO=0" "p1b:TQ_GEMM_PRIO=1" || exit 3
+scripts/ab_env.sh "p0:TQ_GEMM_PRIO=0" "p1:TQ_GEMM_PRIO=1" "l8:TQ_SLICE_LANES=8 TQ_LANE_ARENA_MB=16384" "p0b:TQ_GEMM_PRIO=0" "p1b:TQ_GEMM_PRIO=1" "l8b:TQ_SLICE_LANES=8 TQ_LANE_ARENA_MB=16384" || exit 3
 scripts/prof_round.sh r04
