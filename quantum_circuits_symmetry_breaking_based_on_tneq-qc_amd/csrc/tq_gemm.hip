@@ -1043,6 +1043,44 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       for (int x = 0; x < NTM; ++x) st_lds<KPT>(base + (2 * NTM + x) * sub + toff, t[x]);
     }
   };
+  // development diagnostics (wrong results, realistic operand values: the MFMAs keep multiplying
+  // step 0's real operands, so the chip's power and clock stay those of real data):
+  //  TQ_GEMM_DIAG_NOSTORE: the prologue splits step 0 into BOTH LDS halves, the main loop splits
+  //    every step but stores nothing (the values are kept alive) -- the LDS stores' share
+  //  TQ_GEMM_DIAG_NOREAD: the fragments are read once before the main loop and kept -- the
+  //    fragment reads' share
+  auto keep_split = [&](auto set) {
+    constexpr int S = decltype(set)::value;
+#pragma unroll
+    for (int rw = 0; rw < 2; ++rw) {
+      float re[KPT], im[KPT], sm[KPT];
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        re[j] = rw ? rv[S][j].z : rv[S][j].x;
+        im[j] = rw ? rv[S][j].w : rv[S][j].y;
+        sm[j] = re[j] + im[j];
+      }
+      uint32_t t[NTM][KPT / 2];
+      SP::template split<KPT>(re, sc, t);
+#pragma unroll
+      for (int x = 0; x < NTM; ++x)
+#pragma unroll
+        for (int q = 0; q < KPT / 2; ++q) asm volatile("" ::"v"(t[x][q]));
+      SP::template split<KPT>(im, sc, t);
+#pragma unroll
+      for (int x = 0; x < NTM; ++x)
+#pragma unroll
+        for (int q = 0; q < KPT / 2; ++q) asm volatile("" ::"v"(t[x][q]));
+      if constexpr (G3) {
+        SP::template split<KPT>(sm, sc - 1, t);
+#pragma unroll
+        for (int x = 0; x < NTM; ++x)
+#pragma unroll
+          for (int q = 0; q < KPT / 2; ++q) asm volatile("" ::"v"(t[x][q]));
+      }
+    }
+  };
+  (void)keep_split;
   auto store_stage = [&](auto set, int buf) {
     constexpr int S = decltype(set)::value;
     char* base = lds + buf * BUF + obase;
@@ -1240,8 +1278,24 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       return;
     }
+#ifdef TQ_GEMM_DIAG_NOREAD
+#pragma unroll
+    for (int x = 0; x < NGRP * NTM; ++x) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        asm volatile("" : "+v"(fa[x][i].x), "+v"(fa[x][i].y), "+v"(fa[x][i].z), "+v"(fa[x][i].w));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        asm volatile("" : "+v"(fb[x][j].x), "+v"(fb[x][j].y), "+v"(fb[x][j].z), "+v"(fb[x][j].w));
+    }
+#else
     read_frags(lds + (P & 1) * BUF, fa, fb);
+#endif
+#ifdef TQ_GEMM_DIAG_NOSTORE
+    keep_split(std::integral_constant<int, (P + 1) % NSET>{});
+#else
     store_stage(std::integral_constant<int, (P + 1) % NSET>{}, (P & 1) ^ 1);
+#endif
     mfmas(fa, fb);
     if constexpr (TL::ILV) {
       // fragment reads first, then every MFMA followed by up to 3 VALU (the split, the sign
@@ -1323,7 +1377,13 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   if constexpr (NSET >= 3) load(std::integral_constant<int, NSET >= 3 ? 2 : 0>{}, nkt > 2 ? 2 : nkt - 1);
   if constexpr (NSET >= 4) load(std::integral_constant<int, NSET >= 4 ? 3 : 0>{}, nkt > 3 ? 3 : nkt - 1);
   store_stage(std::integral_constant<int, 0>{}, 0);
+#ifdef TQ_GEMM_DIAG_NOSTORE
+  store_stage(std::integral_constant<int, 0>{}, 1);
+#endif
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifdef TQ_GEMM_DIAG_NOREAD
+  read_frags(lds, fa, fb);
+#endif
   if constexpr (TL::PIPE) read_group(lds, 0, fa, fb);
   int t = 0;
   for (; t + U < nkt; t += U) {
