@@ -343,9 +343,28 @@ def main():
 
     from tneq_qc_amd.distributed import SlicedContraction
     job = SlicedContraction(expr)   # slices rank, rank+N, ... + one RCCL all-reduce (SUM)
+    # N > 1: consecutive steps alternate two output buffers and leave their all-reduce in flight
+    # (async): step k's RCCL reduce overlaps step k + 1's contraction, a buffer is reused only after
+    # its reduce has been waited for; the timed region still ends with a device synchronize
+    bufs = [out, torch.empty_like(out)] if world > 1 else [out]
+    works = [None] * len(bufs)
+    nstep = [0]
 
     def step():
-        job(*ops, out=out)
+        i = nstep[0] % len(bufs)
+        if world > 1:
+            if works[i] is not None:
+                works[i].wait()
+            _, works[i] = job(*ops, out=bufs[i], async_reduce=True)
+        else:
+            job(*ops, out=out)
+        nstep[0] += 1
+
+    def last_out():
+        for w in works:
+            if w is not None:
+                w.wait()
+        return bufs[(nstep[0] - 1) % len(bufs)]
 
     def timed(k: int) -> float:
         torch.cuda.synchronize()
@@ -371,9 +390,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     graphs = plan.query("graph_launches")
-    if args.save_out and rank == 0:
-        import numpy as np
-        np.save(args.save_out, out.cpu().numpy())
+    if args.save_out:
+        res = last_out()
+        if rank == 0:
+            import numpy as np
+            np.save(args.save_out, res.cpu().numpy())
 
     _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step")
     # ---- dominant kernel: the same K steps launched eagerly with HIP events around every GEMM

@@ -29,13 +29,16 @@ def shard_slices(n_slices: int, rank: int, world: int) -> Tuple[int, int, int]:
     return rank, n_slices, world
 
 
-def allreduce_partials(t: torch.Tensor, group=None) -> torch.Tensor:
-    """In-place SUM of a (complex) partial-amplitude buffer across the group (RCCL on GPU)."""
+def allreduce_partials(t: torch.Tensor, group=None, async_op: bool = False):
+    """In-place SUM of a (complex) partial-amplitude buffer across the group (RCCL on GPU).
+    async_op: returns (t, work) -- the collective runs on the process group's stream, after the
+    work already queued on the current stream; `work.wait()` (or a device synchronize) before t
+    is read or written again (work is None at world size 1)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        return t
+        return (t, None) if async_op else t
     view = torch.view_as_real(t) if t.is_complex() else t
-    dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
-    return t
+    work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return (t, work) if async_op else t
 
 
 class AllReduceSum(torch.autograd.Function):
@@ -132,7 +135,10 @@ class SlicedContraction:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.executor = executor
 
-    def __call__(self, *tensors, out: Optional[torch.Tensor] = None):
+    def __call__(self, *tensors, out: Optional[torch.Tensor] = None, async_reduce: bool = False):
+        """async_reduce (plain tensors, no autograd): returns (result, work) with the all-reduce
+        still in flight on the process group's stream -- the next contraction into ANOTHER
+        output buffer overlaps it; `work.wait()` before the result is read or `out` reused."""
         from ..core.tn_tensor import TNTensor
         rng = shard_slices(self.expr.n_slices, self.rank, self.world)
         tn = any(isinstance(t, TNTensor) for t in tensors)
@@ -148,6 +154,8 @@ class SlicedContraction:
             tensors = tuple(raw)
         grad = (torch.is_grad_enabled() and out is None
                 and any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors))
+        if async_reduce and (tn or grad):
+            raise ValueError("async_reduce: plain tensors without autograd only")
         if grad and self.world > 1:
             # replicated operands: their gradients are summed over the ranks in backward
             idx = [i for i, t in enumerate(tensors) if isinstance(t, torch.Tensor) and t.requires_grad]
@@ -169,6 +177,8 @@ class SlicedContraction:
         else:
             part = self.expr(*tensors, out=out, slice_range=rng)
         if not tn:
+            if async_reduce:
+                return allreduce_partials(part, self.group, async_op=True)
             return allreduce_with_grad(part, self.group) if grad else allreduce_partials(part, self.group)
         # normalise the partial (a constant factor: no gradient through the max)
         mx = float(part.detach().abs().max()) if part.numel() else 0.0

@@ -58,9 +58,16 @@ def _worker(rank, world, port, q):
     assert (job.rank, job.world) == (rank, world)
     assert shard_slices(8, rank, world) == (rank, 8, world)
     res = job().numpy()
+    # async reduce (bench.py's pipelined steps): (result, work), the sum lands after work.wait()
+    res2, work = job(async_reduce=True)
+    assert work is not None
+    work.wait()
+    with pytest.raises(ValueError):   # autograd / TNTensor operands keep the synchronous reduce
+        job(torch.ones(1, requires_grad=True), async_reduce=True)
     if rank == 0:
         full = contract(task.eq, *task.operands)
-        q.put(float(np.abs(res - full).max() / np.abs(full).max()))
+        q.put(max(float(np.abs(res - full).max() / np.abs(full).max()),
+                  float(np.abs(res2.numpy() - full).max() / np.abs(full).max())))
     dist.barrier()
     dist.destroy_process_group()
 
