@@ -2622,6 +2622,11 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
           S2Op& o = L.op[L.nops++];
           TQ_TRY(fill_s2(o, op, op.stab1));
           o.lds_io = op.lds_io;
+          // an LDS hand-off moves the whole tensor: the kernel's first-chunk path only
+          if ((o.lds_io & 3) && reinterpret_cast<const S2Desc*>(P.stabs[op.stab1].data())->nchunks != 1) {
+            set_error("internal: sweep2 LDS hand-off on a multi-chunk layout");
+            return TQ_ERR_INVALID;
+          }
           o.block_begin = P.seq_stream[j];   // the stream's workgroup
           o.nblocks = 1;
           ev.flops += op.flops;

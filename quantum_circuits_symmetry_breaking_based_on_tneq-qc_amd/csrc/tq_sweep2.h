@@ -137,9 +137,10 @@ struct S2Op {
 constexpr int kS2SeqMaxStreams = 8;
 struct S2Launch {
   // seq = 0: independent ops (one dependency level), blockIdx ranges select the op; seq = 1:
-  // dependent chains -- workgroup b runs, in order, the ops whose block_begin is b (nblocks 1
-  // each; an op reads only what earlier ops of its own stream wrote): no launch gap between
-  // the small ops of a long chain, and the kernel's code stays in one CU's instruction cache
+  // dependent chains -- workgroup b runs, in order, every op whose range [block_begin,
+  // block_begin + nblocks) holds b (a stream: nblocks 1; an op reads only what earlier ops of
+  // its stream wrote): no launch gap between the small ops of a long chain, and the kernel's
+  // code stays in one CU's instruction cache
   int nops = 0, seq = 0;
   S2Op op[kS2MaxOps];
 };

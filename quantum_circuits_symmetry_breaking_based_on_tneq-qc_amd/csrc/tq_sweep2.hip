@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   __shared__ uint2 keep_raw[sizeof(S2Keep) / 8];          // S2Desc::k, staged once
   // chain launches (S2Launch::seq) with LDS hand-offs: the dynamic LDS holds the tensor an op
   // passes to the next op of its stream, in its memory layout (S2Op::lds_io; <= 64 KiB)
-  extern __shared__ uint2 s2_dyn[];
+  extern __shared__ __attribute__((aligned(16))) uint4 s2_dyn[];   // 16-B slots (complex128)
   Raw* const mir = reinterpret_cast<Raw*>(s2_dyn);
   const S2Keep& keep = *reinterpret_cast<const S2Keep*>(keep_raw);
   const int32_t* const gmeta = &keep.gmeta[0][0];        // K, N, pass mask, kaddr, naddr
@@ -425,7 +425,9 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   Raw pgw[kGt];
   bool have_pf = false;
   for (; j < j_end; ++j) {
-  if (SEQ && L.op[j].block_begin != (int)blockIdx.x) continue;   // another stream's op
+  // another stream's op
+  if (SEQ && ((int)blockIdx.x < L.op[j].block_begin || (int)blockIdx.x >= L.op[j].block_begin + L.op[j].nblocks))
+    continue;
   const S2Op& op = L.op[j];
   const S2Desc* __restrict__ d = op.desc;
 #ifdef TQ_S2_TIMING
@@ -510,7 +512,9 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   TQ_TS(1);
   if constexpr (SEQ) {
     int jn = j + 1;
-    while (jn < L.nops && L.op[jn].block_begin != (int)blockIdx.x) ++jn;
+    while (jn < L.nops && ((int)blockIdx.x < L.op[jn].block_begin ||
+                           (int)blockIdx.x >= L.op[jn].block_begin + L.op[jn].nblocks))
+      ++jn;
     have_pf = jn < L.nops && (L.op[jn].lds_io & 4) != 0;
     if (have_pf) load_desc(L.op[jn], pdw, pgw);
   }
@@ -792,11 +796,12 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
     int streams = 0;
     bool lds = false;
     for (int q = 0; q < L.nops; ++q) {
-      if (L.op[q].block_begin < 0 || L.op[q].block_begin >= kS2SeqMaxStreams || L.op[q].nblocks != 1) {
-        set_error("sweep2: a chain launch runs one workgroup per stream");
+      if (L.op[q].block_begin < 0 || L.op[q].nblocks < 1 ||
+          L.op[q].block_begin + L.op[q].nblocks > kS2SeqMaxStreams) {
+        set_error("sweep2: a chain launch runs at most kS2SeqMaxStreams workgroups");
         return TQ_ERR_INVALID;
       }
-      streams = std::max(streams, L.op[q].block_begin + 1);
+      streams = std::max(streams, L.op[q].block_begin + L.op[q].nblocks);
       lds = lds || L.op[q].lds_io != 0;
     }
     // LDS hand-offs: a 64-KiB dynamic block beside the kernel's ~76 KiB (one workgroup per CU)
