@@ -195,3 +195,45 @@ def test_sgdg_wide_params_low_rank_timed(dev, dtype):
     ms = (time.perf_counter() - t0) / 5 * 1e3
     print(f"SGDG 1 x 2048 {dtype}: {ms:.3f} ms per step")
     assert ms < 50.0, ms
+
+
+@pytest.mark.parametrize("dtype", ["complex128", "float64"])
+def test_sgdg_cached_steady_state_matches_oracle(dev, dtype):
+    """The steady-state path (SGDG caches a group's checks and launch arrays while the
+    parameters, gradients and buffers stay the same tensors -- a training loop whose backward
+    writes the same .grad tensors, e.g. a replayed hipGraph): gradients updated IN PLACE over
+    4 steps match the oracle; then one gradient tensor is replaced (cache miss: the full path)
+    and the state is reset (a new buffer: miss again), still matching.  The retraction draws
+    come from an rng= generator, the oracle draws from an equal one."""
+    import torch
+    from oracle.optim_ref import sgdg_step
+    from tneq_qc_amd.optim import SGDG
+    cplx = dtype.startswith("complex")
+    rng = np.random.default_rng(11)
+    ref = _params(rng, np.dtype(dtype), cplx)
+    params = [torch.nn.Parameter(torch.from_numpy(p.copy()).to(dev)) for p in ref]
+    hp = dict(lr=0.05, momentum=0.9, weight_decay=0.01, nesterov=False, stiefel=True)
+    # a seed whose first draw retracts
+    seed = next(s for s in range(10000) if random.Random(s).randint(1, 101) == 1)
+    opt = SGDG(params, rng=random.Random(seed), **hp)
+    ref_rng = random.Random(seed)
+    state = {}
+    for p in params:
+        p.grad = torch.zeros_like(p)
+    for step in range(7):
+        grads = [(rng.standard_normal(p.shape) + (1j * rng.standard_normal(p.shape) if cplx else 0)).astype(dtype)
+                 for p in ref]
+        if step == 4:        # a new gradient tensor for one parameter: the cache misses
+            params[2].grad = torch.empty_like(params[2])
+        if step == 5:        # the optimizer state reset: new buffers, a miss again
+            opt.state.clear()
+            state.clear()
+        for p, g in zip(params, grads):
+            p.grad.copy_(torch.from_numpy(g.copy()))   # in place: the same .grad tensors
+        opt.step()
+        sgdg_step(ref, [g.copy() for g in grads], state, rng=ref_rng, **hp)
+        torch.cuda.synchronize()
+        for i, (p, r) in enumerate(zip(params, ref)):
+            err = np.abs(p.detach().cpu().numpy() - r).max() / max(np.abs(r).max(), 1e-30)
+            assert err < TOL[dtype], (step, i, err)
+    assert 0 in getattr(opt, "_sgdg_cache", {})   # the steady state was cached
