@@ -205,6 +205,10 @@ int tq_plan_set(tq_plan p, const char* key, int64_t value) {
     p->plan.use_seq = value != 0;
     return TQ_OK;
   }
+  if (k == "sweep_coop") {       // 0: the multi-chunk sweep2 levels of a chain run one launch each
+    p->plan.use_coop = value != 0;
+    return TQ_OK;
+  }
   tq::set_error("tq_plan_set: unknown key " + k);
   return TQ_ERR_INVALID;
 }
@@ -238,9 +242,26 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "n_launch_once") {   // launches of the hoisted part as executed (chain launches merged)
     int64_t c = P.n_launch_once;
     if (P.use_seq) for (auto& r : P.seq_once) c -= r.second - r.first - 1;
+    if (P.use_coop) for (auto& r : P.coop_once) c -= r.second - r.first - 1;
     return c;
   }
   if (k == "n_chain_launches") return P.use_seq ? (int64_t)P.seq_once.size() : 0;
+  if (k == "n_coop_launches") return P.use_coop ? (int64_t)P.coop_once.size() : 0;
+  if (k == "coop_timeouts") {    // waits of cooperative chain launches that gave up (expected 0)
+    int64_t c = 0;
+    for (size_t r = 0; r < P.coop_once.size() && P.d_tables; ++r) {
+      uint32_t w = 0;
+      if (hipMemcpy(&w, (const char*)P.d_tables + P.sync_off + r * tq::Plan::kSyncSlot + 4, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+      c += w;
+    }
+    return c;
+  }
+  if (k == "n_coop_ops") {
+    int64_t c = 0;
+    if (P.use_coop) for (auto& r : P.coop_once) c += r.second - r.first;
+    return c;
+  }
   if (k == "n_launch_slice") return P.n_launch_slice;
   if (k == "out_numel") return P.out_numel;
   return -1;

@@ -328,6 +328,10 @@ class Compiler {
       if (op.kind == OP_SWEEP || op.kind == OP_SWEEP2) P_.n_sweep_gates += (int)op.sgates.size();
     }
     build_schedule();
+    // cooperative chain counters (S2Launch::sync): a 256-byte slot each, behind the other tables
+    // (zero from the upload; every launch leaves its counter at zero)
+    P_.sync_off = P_.table_bytes;
+    P_.table_bytes += P_.coop_once.size() * Plan::kSyncSlot;
     P_.flops = P_.flops_once + P_.flops_slice * (double)P_.n_slices;
     P_.bytes = P_.bytes_once + P_.bytes_slice * (double)P_.n_slices;
     std::ostringstream d;
@@ -349,6 +353,13 @@ class Compiler {
           d << " " << j << "/s" << P_.seq_stream[j] << ((P_.ops[j].lds_io & 1) ? "<" : "")
             << ((P_.ops[j].lds_io & 2) ? ">" : "");
       d << "   (< input from LDS, > result left in LDS)\n";
+    }
+    for (size_t r = 0; r < P_.coop_once.size(); ++r) {
+      d << "# cooperative chain launch (" << P_.coop_width[r]
+        << " workgroups, a counter barrier between ops): once entries " << P_.coop_once[r].first << ".."
+        << P_.coop_once[r].second - 1 << ", ops";
+      for (int i = P_.coop_once[r].first; i < P_.coop_once[r].second; ++i) d << " " << P_.sched_once[i][0];
+      d << "\n";
     }
     P_.describe = d.str();
     return TQ_OK;
@@ -630,6 +641,68 @@ class Compiler {
         P_.ops[k].lds_io |= 1;
       }
     }
+    // cooperative chain launches: consecutive hoisted levels that are each ONE multi-chunk sweep2
+    // op outside a chain launch (C2: 27 levels of 4-chunk ops after its one-chunk chain) run as
+    // one launch of n workgroups, every op's chunks spread over all of them and a counter barrier
+    // between consecutive ops (S2Launch::sync).  Plain ops only (no beta / max / split / output:
+    // their stores and loads are the coherent forms), and no op of a run writes a gate tensor of
+    // the run (gates are read through the caches, and prefetched)
+    P_.coop_once.clear();
+    P_.coop_width.clear();
+    P_.use_coop = s2_coop_enabled();
+    std::vector<char> in_chain(ns, 0);
+    for (auto& r : P_.seq_once)
+      for (int i = r.first; i < r.second; ++i) in_chain[i] = 1;
+    auto coop_ok = [&](int i) {
+      if (in_chain[i] || P_.sched_once[i].size() != 1) return false;
+      const Op& op = P_.ops[P_.sched_once[i][0]];
+      return op.kind == OP_SWEEP2 && !op.s2_dense && !op.writes_output && op.amax_word < 0 && op.ps_gemm < 0 &&
+             op.s2_nchunks >= 2 && op.s2_nchunks <= s2_coop_max_chunks();
+    };
+    for (int i = 0; i < ns;) {
+      if (!coop_ok(i)) { ++i; continue; }
+      std::vector<Acc> gates, writes;
+      int e = i;
+      for (; e < ns && coop_ok(e) && e - i < kS2MaxOps; ++e) {
+        const int j = P_.sched_once[e][0];
+        std::vector<Acc> g;
+        for (auto& sg : P_.ops[j].sgates) add(g, sg.g, sg.n);
+        if (overlap(wr[j], gates) || overlap(writes, g) || overlap(wr[j], g)) break;
+        gates.insert(gates.end(), g.begin(), g.end());
+        writes.insert(writes.end(), wr[j].begin(), wr[j].end());
+      }
+      if (e - i >= 2) {
+        // workgroups: the most common chunk count of the run (an op of more chunks strides them)
+        std::vector<int> cnt(17, 0);
+        for (int q = i; q < e; ++q) ++cnt[(int)P_.ops[P_.sched_once[q][0]].s2_nchunks];
+        int w = 2;
+        for (int c = 2; c <= 16; ++c) if (cnt[c] > cnt[w]) w = c;
+        P_.coop_once.push_back({i, e});
+        P_.coop_width.push_back(std::min(w, kS2SeqMaxStreams));
+        // the next op's descriptor and gates prefetched (no op of the run writes a gate of it)
+        for (int q = i; q < e; ++q) P_.ops[P_.sched_once[q][0]].lds_io = s2_seq_prefetch() ? 4 : 0;
+      }
+      i = std::max(e, i + 1);
+    }
+  }
+  // cooperative chain launches (TQ_S2_COOP=1, default 0; tq_plan_set "sweep_coop") for levels of
+  // ops of at most TQ_S2_COOPCH chunks (default 16).  Measured r04 (C2, complex64, 26 levels in
+  // one launch of 4 workgroups): 0.379 ms against 0.363 one launch per level -- the launch gaps
+  // it removes (~1.7 us each, 46 us in all) come back as longer ops (write-through stores
+  // drained before the arrival, the poll, L2-missing loads: +1.1 us per op), so it is off
+  static bool s2_coop_enabled() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_COOP");
+      return e && e[0] == '1';
+    }();
+    return v;
+  }
+  static int s2_coop_max_chunks() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_COOPCH");
+      return e ? std::min(16, atoi(e)) : 16;
+    }();
+    return v;
   }
   // chain launches take small ops of at most this many chunks, in their one-chunk layout
   // (TQ_S2_SEQCH, default 2).  Measured r04: C2's 29 levels of 4-chunk ops as one chain are
@@ -2370,6 +2443,7 @@ int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, 
   key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
   key.mode = P.run_mode;
   key.seq = P.use_seq;
+  key.coop = P.use_coop;
   constexpr size_t kMaxGraphs = 8;
   Plan::GraphEntry* hit = nullptr;
   for (auto& g : P.graphs) if (g.key == key) hit = &g;
@@ -2599,8 +2673,9 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
       return TQ_OK;
     };
-    // Plan::seq_once run [b, e): its ops in order, one workgroup, one launch
-    auto launch_chain = [&](int b, int e) -> int {
+    // Plan::seq_once run [b, e): its ops in order, a workgroup per stream, one launch; or
+    // (coop >= 0) Plan::coop_once run `coop`: its ops in order on coop_width workgroups each
+    auto launch_chain = [&](int b, int e, int coop) -> int {
       Plan::Ev ev{};
       const bool prof = (P.profile >> (int)OP_SWEEP) & 1;
       if (prof) {
@@ -2616,6 +2691,28 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       }
       S2Launch L;
       L.seq = 1;
+      if (coop >= 0) {
+        const int w = P.coop_width[coop];
+        L.sync = reinterpret_cast<uint32_t*>((char*)P.d_tables + P.sync_off + (size_t)coop * Plan::kSyncSlot);
+        for (int i = b; i < e; ++i) {
+          const Op& op = P.ops[P.sched_once[i][0]];
+          S2Op& o = L.op[L.nops];
+          TQ_TRY(fill_s2(o, op, op.stab));
+          o.block_begin = 0;
+          o.nblocks = w;
+          o.lds_io = kS2Coop | (L.nops * w) << 8 | (op.lds_io & 4);   // (bit 2: set by the planner)
+          ++L.nops;
+          ev.flops += op.flops;
+          ev.bytes += op.bytes;
+        }
+        L.sync_total = L.nops * w;
+        TQ_TRY(sweep2_launch(P.dtype, L, stream));
+        if (prof) {
+          TQ_HIP(hipEventRecord(ev.b, stream));
+          P.ev_used.push_back(ev);
+        }
+        return TQ_OK;
+      }
       for (int i = b; i < e; ++i)
         for (int j : P.sched_once[i]) {
           const Op& op = P.ops[j];
@@ -2739,12 +2836,18 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     };
     if (sl == s_begin) {
       if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
-      size_t run = 0;
+      size_t run = 0, crun = 0;
       for (int i = 0; i < (int)P.sched_once.size();) {
         while (P.use_seq && run < P.seq_once.size() && P.seq_once[run].first < i) ++run;
         if (P.use_seq && run < P.seq_once.size() && P.seq_once[run].first == i) {
-          TQ_TRY(launch_chain(i, P.seq_once[run].second));
+          TQ_TRY(launch_chain(i, P.seq_once[run].second, -1));
           i = P.seq_once[run].second;
+          continue;
+        }
+        while (P.use_coop && crun < P.coop_once.size() && P.coop_once[crun].first < i) ++crun;
+        if (P.use_coop && crun < P.coop_once.size() && P.coop_once[crun].first == i) {
+          TQ_TRY(launch_chain(i, P.coop_once[crun].second, (int)crun));
+          i = P.coop_once[crun].second;
           continue;
         }
         TQ_TRY(launch(P.sched_once[i]));

@@ -172,6 +172,16 @@ struct Plan {
   std::vector<std::pair<int, int>> seq_once;
   std::vector<int> seq_stream;   // per op: its stream (workgroup) in a chain launch, -1 none
   bool use_seq = true;
+  // cooperative chain launches: runs [first, last) of consecutive sched_once entries that are
+  // each ONE multi-chunk sweep2 op (C2's 27 levels of 4-chunk ops), run by coop_width[r]
+  // workgroups in one launch with a counter barrier between the ops (S2Launch::sync = the
+  // 256-byte slot r at sync_off of the tables) when use_coop (env TQ_S2_COOP; tq_plan_set
+  // "sweep_coop")
+  static constexpr size_t kSyncSlot = 256;
+  std::vector<std::pair<int, int>> coop_once;
+  std::vector<int> coop_width;
+  size_t sync_off = 0;
+  bool use_coop = true;
   std::string describe;
   // hipGraph of the whole launch sequence of one execute call, replayed while the call's
   // pointers / slice range / flags are unchanged (a plan is hundreds of small launches)
@@ -182,9 +192,10 @@ struct Plan {
     int acc = 0;
     int mode = 0;   // Plan::run_mode the graph was captured with
     bool seq = true;  // Plan::use_seq
+    bool coop = true;  // Plan::use_coop
     bool operator==(const GraphKey& o) const {
       return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc &&
-             mode == o.mode && seq == o.seq;
+             mode == o.mode && seq == o.seq && coop == o.coop;
     }
   };
   bool use_graph = true;

@@ -122,7 +122,9 @@ struct S2Op {
   // dynamic LDS block (left there by the previous op of this stream), bit 1 = Y goes there
   // instead of memory (the next op of this stream is its only reader; no beta, no split, no max),
   // bit 2 = no op of the launch writes this op's gate tensors (its descriptor and gate elements
-  // may be loaded while the previous op of its stream runs)
+  // may be loaded while the previous op of its stream runs), bit 3 (kS2Coop) = a cooperative op
+  // (S2Launch::sync): its X / Y move through L2-coherent accesses, and bits 8.. hold the count of
+  // arrivals it waits for before its loads (every workgroup of the launch arrives once per op)
   int use_beta = 0, lds_io = 0;
   // complex64 only, optional: the op atomically max-es the float bits of max |re|, |im| over
   // every value it stores into *amax (zeroed before; the max a consuming f16-split GEMM scales by)
@@ -135,6 +137,7 @@ struct S2Op {
 
 // streams of a chain launch (S2Launch::seq), a workgroup each
 constexpr int kS2SeqMaxStreams = 8;
+constexpr int kS2Coop = 8;   // S2Op::lds_io: a cooperative op
 struct S2Launch {
   // seq = 0: independent ops (one dependency level), blockIdx ranges select the op; seq = 1:
   // dependent chains -- workgroup b runs, in order, every op whose range [block_begin,
@@ -142,6 +145,14 @@ struct S2Launch {
   // its stream wrote): no launch gap between the small ops of a long chain, and the kernel's
   // code stays in one CU's instruction cache
   int nops = 0, seq = 0;
+  // cooperative chain (seq = 1, every op kS2Coop over the same workgroups [0, n)): op k's
+  // chunks are spread over the n workgroups, and op k + 1 reads what ANY of them stored, so a
+  // counter barrier separates the ops: every workgroup adds 1 to sync[0] after its op-k stores
+  // have completed, and loads op k + 1's input once sync[0] >= (k + 1) n.  sync[0] is zero when
+  // the launch starts; the last arrival (sync_total = ops x n) resets it.  sync[1] counts
+  // waits that gave up (a bounded spin: never expected; the results are then invalid)
+  uint32_t* sync = nullptr;
+  int sync_total = 0, pad = 0;
   S2Op op[kS2MaxOps];
 };
 

@@ -64,7 +64,7 @@ static_assert(kLut == 64, "lut layout shared with S2Desc::lut");
 // wall-clock stamps (100 MHz) at its phase boundaries
 // record: [0..6] phase stamps, [7] blocks|chunks, [8] first chunk's gate clocks,
 // [9..24] clock at the end of each pass of the first chunk, [25..40] pass kind (B<<16|K<<8|N)
-constexpr int kTsMax = 2048, kTsPh = 44;   // [41..43]: sub-stamps of the tables phase
+constexpr int kTsMax = 2048, kTsPh = 48;   // [41..47]: sub-stamps of the tables phase
 __device__ unsigned long long g_s2_ts[kTsMax][kTsPh];
 __device__ unsigned int g_s2_seq;
 #define TQ_TS(ph) do { if (ts_rec && threadIdx.x == 0) g_s2_ts[ts_idx][ph] = wall_clock64(); } while (0)
@@ -105,6 +105,47 @@ template <typename T>
 __device__ __forceinline__ const T* lane_at(const T* base, uint32_t byte_off) {
   return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
+
+// Cooperative chain ops (S2Launch::sync): a tensor one workgroup stores and another loads in the
+// same launch moves through vector buffer accesses with the sc1 policy (write-through stores,
+// L1-bypassing loads, coherent across the XCDs' L2s), one element per lane -- the hand-off form the
+// MI355X guide measures valid with a counter between them (stores drained by every wave, a
+// workgroup barrier, one agent-scope add; one polling lane, a barrier, then the loads).
+// `base` is wave-uniform (the buffer descriptor is built in scalar registers), `off` the lane's
+// byte offset.
+constexpr int kSc1 = 16;   // cache-policy bits of a buffer access: sc1
+template <typename W>
+__device__ __forceinline__ W ld_coherent(const void* base, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+  if constexpr (sizeof(W) == 16) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1);
+    return __builtin_bit_cast(W, v);
+  } else if constexpr (sizeof(W) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kSc1);
+    return __builtin_bit_cast(W, v);
+  } else {
+    static_assert(sizeof(W) == 4, "4-, 8- or 16-byte elements");
+    const auto v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSc1);
+    return __builtin_bit_cast(W, v);
+  }
+}
+template <typename W>
+__device__ __forceinline__ void st_coherent(void* base, uint32_t off, const W& w) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, -1, 0x00020000);
+  if constexpr (sizeof(W) == 16) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int __attribute__((ext_vector_type(4))), w), r, off, 0,
+                                           kSc1);
+  } else if constexpr (sizeof(W) == 8) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(int __attribute__((ext_vector_type(2))), w), r, off, 0,
+                                          kSc1);
+  } else {
+    static_assert(sizeof(W) == 4, "4-, 8- or 16-byte elements");
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, w), r, off, 0, kSc1);
+  }
+}
+// bounded polls of a cooperative chain's counter (~1 s): a lost arrival cannot hang the GPU
+constexpr int kCoopSpin = 1 << 20;
 
 // acc += a * b on packed f32: (a.re, a.re) * (b.re, b.im) + (a.im, a.im) * (-b.im, b.re).
 // The broadcasts and the swap / negation are operand modifiers (op_sel / neg), not copies.
@@ -405,6 +446,15 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   if (SEQ) j = 0;
   // descriptor words / gate-tensor elements per thread of the coalesced staging copy
   constexpr int kIt = (kDescWords2 + NT - 1) / NT, kGt = (kS2MaxGates * kS2GateRaw + NT - 1) / NT;
+  // elements of gate gi (wave-uniform) an op stages: S2Op::gnum through the scalar unit (its
+  // dword: no byte loads there) -- a per-lane index made it a vector load of the argument block,
+  // waited for (with every load in flight) before the gate elements could be requested
+  using KArg = const __attribute__((address_space(4))) S2Op*;
+  using KWord = const __attribute__((address_space(4))) uint32_t*;
+  auto gate_count = [](const S2Op& o, int gi) {
+    const KArg ko = (KArg)&o;
+    return gi < kS2MaxGates ? (int)((((KWord)ko->gnum)[gi >> 2] >> ((gi & 3) * 8)) & 0xff) : 0;
+  };
   auto load_desc = [&](const S2Op& o, uint2 (&w)[kIt], Raw (&g)[kGt]) {
     const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(o.desc);
 #pragma unroll
@@ -412,11 +462,15 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
       const int i = tid + it * NT;
       if (i < kDescWords2) w[it] = gd[i];
     }
+    // gate gi = (i / kS2GateRaw) is wave-uniform (kS2GateRaw = the wave size): its element count
+    // and pointer come from the kernel argument through the scalar cache
+    static_assert(kS2GateRaw == 64 && NT % 64 == 0, "one gate per wave and slot");
+    const KArg ko = (KArg)&o;
 #pragma unroll
     for (int it = 0; it < kGt; ++it) {
       const int i = tid + it * NT;
-      const int gi = i / kS2GateRaw, e = i % kS2GateRaw;
-      if (i < kS2MaxGates * kS2GateRaw && e < (int)o.gnum[gi]) g[it] = reinterpret_cast<const Raw*>(o.G[gi])[e];
+      const int gi = __builtin_amdgcn_readfirstlane(i / kS2GateRaw), e = i % kS2GateRaw;
+      if (e < gate_count(o, gi)) g[it] = reinterpret_cast<const Raw*>(ko->G[gi])[e];
     }
   };
   // SEQ: the next op of this stream's descriptor and gate elements, loaded into registers while
@@ -472,8 +526,8 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
 #pragma unroll
     for (int it = 0; it < kGt; ++it) {
       const int i = tid + it * NT;
-      const int g = i / kS2GateRaw, e = i % kS2GateRaw;
-      if (i < kS2MaxGates * kS2GateRaw && e < (int)op.gnum[g]) reinterpret_cast<Raw*>(graw)[i] = gw[it];
+      const int g = __builtin_amdgcn_readfirstlane(i / kS2GateRaw), e = i % kS2GateRaw;
+      if (e < gate_count(op, g)) reinterpret_cast<Raw*>(graw)[i] = gw[it];
     }
   }
   const T* __restrict__ X = reinterpret_cast<const T*>(op.X);
@@ -488,6 +542,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   const bool use_beta = op.use_beta;
   const double beta = op.beta;
   const bool x_lds = SEQ && (op.lds_io & 1) != 0, y_lds = SEQ && (op.lds_io & 2) != 0;   // chain hand-offs
+  const bool coop = SEQ && (op.lds_io & kS2Coop) != 0;   // cooperative chain (S2Launch::sync)
   // producer-side max of a complex64 GEMM operand (S2Op::amax): max |re|, |im| of the values
   // this thread stores, one atomic per wave after the chunk loop
   constexpr bool kC64 = std::is_same<T, c64>::value;
@@ -518,6 +573,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     have_pf = jn < L.nops && (L.op[jn].lds_io & 4) != 0;
     if (have_pf) load_desc(L.op[jn], pdw, pgw);
   }
+  TQ_TS(44);   // next descriptor's loads issued
   const S2Desc* ds = reinterpret_cast<const S2Desc*>(buf);
   const int ngates = ds->ngates;
   const int epi = ds->epi;   // S2Desc::epi (read before the tile overwrites the descriptor copy)
@@ -538,6 +594,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
       sta ^= sb_on ? sa : 0;
     }
   }
+  TQ_TS(45);   // lane offsets
   const bool st_lane = tid < nout;
   // uniform part (chunk + register slot) in scalar registers, lane part as a 32-bit byte offset
   const uint32_t ldo = (uint32_t)(ldm * (int64_t)sizeof(T)), sto = (uint32_t)(stm * (int64_t)sizeof(T));
@@ -556,17 +613,23 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   {
     const int64_t chl = lb + (int64_t)(tid & 63) * nb;
     for (int b0 = logC & ~7; b0 < colbits; b0 += 8) {   // batches of 8 weights in flight
+      int64_t wi[8], wo[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // every read issued before the first is used
+        const int bb = b0 + q < kS2MaxColBits ? b0 + q : kS2MaxColBits - 1;
+        wi[q] = keep.w_in[bb];
+        wo[q] = keep.w_out[bb];
+      }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int b = b0 + q;
-        const int bb = b < kS2MaxColBits ? b : kS2MaxColBits - 1;
-        const int64_t wi = keep.w_in[bb], wo = keep.w_out[bb];
         const bool on = b >= logC && b < colbits && ((chl >> (b - logC)) & 1);
-        cb_in += on ? wi : 0;
-        cb_out += on ? wo : 0;
+        cb_in += on ? wi[q] : 0;
+        cb_out += on ? wo[q] : 0;
       }
     }
   }
+  TQ_TS(46);   // chunk bases
   auto lane64 = [](int64_t v, int i) {
     const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, i);
     const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), i);
@@ -600,6 +663,10 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   auto prefetch = [&](int i, int64_t ch) {
     if (!pf) return;
     const int64_t base = base_in(i, ch);
+    if (coop) {
+      TQ_BY_COUNT(RPF, rin, reg[r] = ld_coherent<Raw>(Xr + uniform(base + keep.ld_hm[r]), ldo));
+      return;
+    }
     TQ_BY_COUNT(RPF, rin, reg[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
   };
   auto fill = [&](int i, int64_t ch) {   // the chunk's elements -> tile
@@ -609,10 +676,27 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     }
     const int64_t base = base_in(i, ch);
     Raw t[RMAX];
-    TQ_BY_COUNT(RMAX, rin, t[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
+    if (coop) TQ_BY_COUNT(RMAX, rin, t[r] = ld_coherent<Raw>(Xr + uniform(base + keep.ld_hm[r]), ldo));
+    else TQ_BY_COUNT(RMAX, rin, t[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
     TQ_BY_COUNT(RMAX, rin, bufr[lda ^ keep.ld_ha[r]] = t[r]);
   };
   Raw reg0[RMAX];
+  // ---- a cooperative op waits for every workgroup's arrival after the previous ops (their
+  // stores complete): one lane polls the counter, the others wait at the barrier.  Every
+  // workgroup waits, one with no chunk of this op too, so the count cannot run ahead of a slow one
+  if constexpr (SEQ) {
+    const uint32_t need = (uint32_t)op.lds_io >> 8;
+    if (coop && need) {
+      if (tid == 0) {
+        int n = 0;
+        while (__hip_atomic_load(L.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need && ++n < kCoopSpin)
+          __builtin_amdgcn_s_sleep(2);
+        if (n == kCoopSpin) __hip_atomic_fetch_add(L.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    }
+  }
+  TQ_TS(47);   // cooperative wait
   // ---- the first chunk's loads go out now (addresses from the staged descriptor) and land
   // while the tables are staged
   int64_t ch = lb;
@@ -621,6 +705,8 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     if (x_lds) {   // the previous op of this stream left the tensor in LDS (one chunk)
       const int lm = (int)ldm;
       TQ_BY_COUNT(RMAX, rin, reg0[r] = mir[(int)(base + keep.ld_hm[r]) + lm]);
+    } else if (coop) {
+      TQ_BY_COUNT(RMAX, rin, reg0[r] = ld_coherent<Raw>(Xr + uniform(base + keep.ld_hm[r]), ldo));
     } else {
       TQ_BY_COUNT(RMAX, rin, reg0[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
     }
@@ -692,6 +778,9 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
           if (st_lane && y_lds) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) reinterpret_cast<T*>(mir)[(int)(base + keep.st_hm[r0 + q]) + (int)stm] = t[q];
+          } else if (st_lane && coop) {   // (no beta, no split, no max: the planner's cooperative ops)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) st_coherent(Y + uniform(base + keep.st_hm[r0 + q]), sto, t[q]);
           } else if (st_lane) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -708,6 +797,8 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
         TQ_BY_COUNT(4, rout, t[r] = buf[sta ^ keep.st_ha[r]]);
         if (st_lane && y_lds) {
           TQ_BY_COUNT(4, rout, reinterpret_cast<T*>(mir)[(int)(base + keep.st_hm[r]) + (int)stm] = t[r]);
+        } else if (st_lane && coop) {
+          TQ_BY_COUNT(4, rout, st_coherent(Y + uniform(base + keep.st_hm[r]), sto, t[r]));
         } else if (st_lane) {
           TQ_BY_COUNT(4, rout, {
             T* p = lane_at(Y + uniform(base + keep.st_hm[r]), sto);
@@ -746,6 +837,10 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
               reinterpret_cast<T*>(mir)[(int)(base + keep.st_hm[r0 + n]) + (int)stm] = acc;
               continue;
             }
+            if (coop) {
+              st_coherent(Y + uniform(base + keep.st_hm[r0 + n]), sto, acc);
+              continue;
+            }
             T* p = lane_at(Y + uniform(base + keep.st_hm[r0 + n]), sto);
             const T v = use_beta ? scale_add(acc, *p, beta) : acc;
             TQ_ST(p, stored(v));
@@ -772,6 +867,18 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     if (ch == lb) TQ_TS(5);
     if (more) fill(i + 1, nxt);
     __syncthreads();
+  }
+  // a cooperative op's arrival: every wave's stores have completed (vmcnt(0)), then the
+  // workgroup barrier, then one agent-scope add; the launch's last arrival resets the counter
+  if constexpr (SEQ) {
+    if (coop) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      if (tid == 0) {
+        const uint32_t n = __hip_atomic_fetch_add(L.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n + 1 == (uint32_t)L.sync_total) __hip_atomic_store(L.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   if (amax) {
 #pragma unroll
@@ -804,7 +911,23 @@ int launch_t(const S2Launch& L, hipStream_t stream) {
       streams = std::max(streams, L.op[q].block_begin + L.op[q].nblocks);
       lds = lds || L.op[q].lds_io != 0;
     }
-    // LDS hand-offs: a 64-KiB dynamic block beside the kernel's ~76 KiB (one workgroup per CU)
+    // a cooperative chain: every op on all the launch's workgroups, op k waiting for k x n
+    // arrivals, no LDS hand-off (a mixed launch could strand a workgroup at a wait)
+    int ncoop = 0;
+    for (int q = 0; q < L.nops; ++q) ncoop += (L.op[q].lds_io & kS2Coop) != 0;
+    if (ncoop) {
+      bool ok = ncoop == L.nops && L.sync != nullptr && L.sync_total == ncoop * streams;
+      for (int q = 0; q < L.nops && ok; ++q)
+        ok = L.op[q].block_begin == 0 && L.op[q].nblocks == streams && (L.op[q].lds_io & 3) == 0 &&
+             (L.op[q].lds_io >> 8) == q * streams && !L.op[q].use_beta && !L.op[q].amax && !L.op[q].split_sc;
+      if (!ok) {
+        set_error("sweep2: malformed cooperative chain launch");
+        return TQ_ERR_INVALID;
+      }
+    }
+    // LDS hand-offs: a 64-KiB dynamic block beside the kernel's ~76 KiB (one workgroup per CU;
+    // every cooperative chain takes it too: the sc1 hand-off between its workgroups is the form
+    // measured with one workgroup per CU)
     const unsigned dyn = lds ? (unsigned)kS2ChunkBytes : 0u;
     if (dyn) {
       static DeviceCache<1> attr;

@@ -57,7 +57,8 @@ class NativePlan:
 
     def set(self, key: str, value: int) -> None:
         """Plan option (tq_plan_set): "graph" (replay a captured hipGraph, default 1),
-        "sweep_chain" (chain launches of small dependent sweep2 ops, default 1)."""
+        "sweep_chain" (chain launches of small dependent sweep2 ops, default 1), "sweep_coop"
+        (cooperative launches of dependent multi-chunk sweep2 levels, default 1)."""
         check(_lib.lib().tq_plan_set(self._h, key.encode(), int(value)), "tq_plan_set")
 
     def describe(self) -> str:

@@ -16,7 +16,7 @@ L = _lib.lib()
 f = L.tq_debug_sweep2_timing
 f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 f.restype = ctypes.c_int
-NREC, W = 2048, 44
+NREC, W = 2048, 48
 buf = (ctypes.c_ulonglong * (NREC * W))()
 task = config_task(sys.argv[1] if len(sys.argv) > 1 else "C4")
 expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
@@ -51,6 +51,14 @@ for r in a:
     if min(t41, t42, t43) > 0:
         sub += np.array([t41 - t1, t42 - t41, t43 - t42, t2 - t43]) / 100.0
 print("tables phase split (sum, us):", json.dumps(dict(zip(["lane_offs+chunk0_issue", "coeffs", "tables", "barrier"], np.round(sub, 1).tolist()))))
+# the first part in detail (stamps 44-47: next descriptor issued, lane offsets, chunk bases,
+# cooperative wait; 41: first chunk's loads issued)
+sub = np.zeros(5)
+for r in a:
+    t = [r[1], r[44], r[45], r[46], r[47], r[41]]
+    if min(t) > 0:
+        sub += np.diff(np.array(t)) / 100.0
+print("lane_offs+chunk0_issue split (sum, us):", json.dumps(dict(zip(["next_desc_issue", "lane_offsets", "chunk_bases", "coop_wait", "chunk0_issue"], np.round(sub, 1).tolist()))))
 # per-pass clocks of the first chunk (shader clock), grouped by pass kind
 kinds = {}
 for r in a:

@@ -74,6 +74,34 @@ def test_chain_launch_equals_one_launch_per_level(dev, cfg):
         assert np.abs(a - b).max() <= tol * np.abs(b).max() and np.array_equal(a, c)
 
 
+def test_cooperative_chain_equals_one_launch_per_level(dev):
+    """C2's 26 levels of one multi-chunk sweep2 op run as ONE cooperative launch with
+    "sweep_coop" = 1 (complex64: 4 workgroups; complex128, twice the chunks: 8 workgroups, 32 + 2
+    ops), each op's chunks spread over them, a counter barrier between the ops, sc1 loads /
+    stores: tq_plan.cpp Plan::coop_once, S2Launch::sync); "sweep_coop" = 0 (the default, measured
+    faster) launches them level by level.  Same descriptors, same arithmetic: the results are bit-identical, on every one of many
+    graph replays (a missed barrier shows up as a stale chunk), eager and captured, and no wait
+    gave up."""
+    import torch
+    from tneq_qc_amd.circuits import config_task
+    t = config_task("C2")
+    for dt in (torch.complex128, torch.complex64):
+        e, ops = _expr_and_ops(t, dev, dt)
+        p = e.plan(dt)
+        p.set("sweep_coop", 1)
+        assert p.query("n_coop_launches") >= 1 and p.query("n_coop_ops") >= 20   # c128: 32 + 2 ops
+        p.set("sweep_coop", 0)
+        ref = e(*ops).cpu().numpy()
+        p.set("sweep_coop", 1)
+        refd = torch.from_numpy(ref).to(dev)
+        for graph in (1, 0):
+            p.set("graph", graph)
+            bad = sum(int(not torch.equal(e(*ops), refd)) for _ in range(40))
+            assert bad == 0, (dt, graph, bad)
+        p.set("graph", 1)
+        assert p.query("coop_timeouts") == 0
+
+
 _ORACLE_SLICES = {}
 
 

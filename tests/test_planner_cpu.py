@@ -262,6 +262,28 @@ def test_small_hoisted_levels_run_as_one_chain_launch():
         p.set("sweep_chain", 1)
 
 
+def test_multi_chunk_hoisted_levels_run_as_one_cooperative_launch():
+    """C2's hoisted levels of one multi-chunk sweep2 op each (after its one-chunk chain) form
+    ONE cooperative launch of 4 workgroups (its most common chunk count) with a counter barrier
+    between the ops (tq_plan.cpp Plan::coop_once), run when "sweep_coop" = 1 (measured slower,
+    so off by default: one launch per level).  C3 / C4 have no such run (their multi-chunk levels
+    hold several ops or are per slice)."""
+    e, p = _plan(config_task("C2"))
+    assert p.query("n_coop_launches") == 0   # off by default
+    p.set("sweep_coop", 1)
+    d = [l for l in p.describe().splitlines() if l.startswith("# cooperative chain launch")]
+    assert len(d) == 1 and "(4 workgroups" in d[0], d
+    ops = [int(x) for x in d[0].split(", ops")[1].split()]
+    assert ops == list(range(ops[0], ops[0] + len(ops))) and len(ops) >= 20
+    assert p.query("n_coop_launches") == 1 and p.query("n_coop_ops") == len(ops)
+    n_on = p.query("n_launch_once")
+    p.set("sweep_coop", 0)
+    assert p.query("n_coop_launches") == 0 and p.query("n_launch_once") == n_on + len(ops) - 1
+    p.set("sweep_coop", 1)
+    for cfg in ("C3", "C4"):
+        assert _plan(config_task(cfg))[1].query("n_coop_launches") == 0
+
+
 @pytest.mark.parametrize("cfg", ["C3", "C4"])
 def test_lane_batched_boundary_gemm_and_lane_sum(cfg):
     """With slice lanes the boundary GEMM (lane-local operands) is one batched launch per batch
