@@ -1635,8 +1635,14 @@ class Compiler {
         uint32_t bm = 0, live = 0;
         const int e = block_span(j, ng, &bm, &live);
         if (e - j < 2) {
-          pm[kS2PmCount] = 1;
+          // a single-gate pass carries the gate's fields itself (S2Keep::pmeta): the kernel
+          // reads a pass's whole head in one batch, ahead of the pass
+          const S2Gate& G = d.gate[j];
+          pm[kS2PmCount] = 1 | ((G.K * 16 + G.N) << 8);
           pm[kS2PmB] = 0;
+          pm[kS2PmPass] = (int32_t)G.pass_mask;
+          for (int k = 0; k < kS2MaxK; ++k) pm[kS2PmAddr + k] = k < G.K ? G.kaddr[k] : 0;
+          for (int n = 0; n < kS2MaxKN; ++n) pm[kS2PmCode + n] = n < G.N ? G.naddr[n] : 0;
           j += 1;
           continue;
         }
@@ -1677,6 +1683,12 @@ class Compiler {
         }
         group_lut(live & ~bm, d.k.lut[j]);
         j = e;
+      }
+      // group tables by pass (row p = the table of pass p's first gate): the kernel reads a
+      // pass's row without first reading which gate starts it
+      for (int q = 0; q < d.npass; ++q) {
+        const int g = d.k.pmeta[q][kS2PmFirst];
+        if (g != q) std::copy(d.k.lut[g], d.k.lut[g] + 64, d.k.lut[q]);
       }
     }
     if (getenv("TQ_DEBUG_S2")) {

@@ -55,7 +55,7 @@ struct S2Keep {
   int64_t w_in[kS2MaxColBits] = {}, w_out[kS2MaxColBits] = {};  // column-bit weights
   int32_t ld_ha[kS2MaxSlots] = {}, st_ha[kS2MaxSlots] = {};
   // Built on the host (plan compile):
-  //  lut[g][j]: LDS BYTE offset part of group index bits -> ((pass positions << logC) ^ swizzle)
+  //  lut[p][j]: LDS BYTE offset part of group index bits -> ((pass positions << logC) ^ swizzle)
   //             * element size, j < 32 for the low 5 pass bits, 32 + j for the high ones
   //             (XOR-linear, combined by ^)
   //  gmeta[g][f]: K, N, pass mask, kaddr[0..3], naddr[0..7] (kS2GmK.. layout; element units)
@@ -67,8 +67,10 @@ struct S2Keep {
   // run to them (one LDS read + write per element for the run instead of per gate).
   //  pmeta[p]: first gate, gate count, B (0 = single gate), pass mask (live positions outside the
   //            block), block-bit address parts [4, 4+B), per-gate local codes [8, 8+count):
-  //            bits 0-1 / 2-3 = block bits of the gate's index bits 0 / 1, bit 4 = 4x4 (else 2x2)
-  //  a block's group table replaces lut[first gate]
+  //            bits 0-1 / 2-3 = block bits of the gate's index bits 0 / 1, bit 4 = 4x4 (else 2x2).
+  //            A single-gate pass (B = 0) carries its gate instead: count | (K*16+N) << 8, the
+  //            gate's pass mask, kaddr [4, 8), naddr [8, 16) -- a pass's head is one read batch
+  //  lut rows are by PASS (row p: the group table of pass p; a block's own table)
   int32_t pmeta[kS2MaxGates][16] = {};
 };
 

@@ -197,13 +197,21 @@ __device__ __forceinline__ void mac(T& acc, const T& a, const T& b) {
   }
 }
 
+// A pass's head (S2Keep::pmeta row, wave-uniform, in scalar registers): everything a pass needs
+// before its element addresses.  One batch of LDS reads, issued together with the pass's group
+// table reads (rows by pass), so a pass is head + table -> elements -> barrier: two dependent
+// LDS round trips where it was four (r04: ~2600 clocks per pass on tiny chunks -- pass row, gate
+// row, group table, elements, and the barrier).
+struct PassHead {
+  int32_t w[16];   // pmeta row: first gate, count (| K*16+N << 8 for a single gate), B, pass mask, ...
+};
+
 // One gate over all groups of the chunk.  Every LDS address is an XOR of contributions:
 // group (lut[pp] ^ c) ^ input k (kaddr[k]) / output n (naddr[n]).  U groups per thread in
 // flight; all K inputs of a group are read before any of its N outputs is written (outputs
 // reuse the input positions).
 template <typename T, int K, int N>
-__device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restrict__ cf,
-                                          const int32_t* __restrict__ gm,
+__device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restrict__ cf, const PassHead& h,
                                           const int32_t* __restrict__ lut, int logC) {
   constexpr int U = sizeof(T) > 8 ? (K * N >= 8 ? 1 : 2) : (K * N >= 16 ? 2 : 4);
   // coefficients held in registers (up to 32 VGPRs for FP32 data, 16 for FP64); larger gates
@@ -212,13 +220,14 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
   constexpr int SH = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;   // element -> byte offset
   char* const bb = reinterpret_cast<char*>(buf);
   const int tid = threadIdx.x;
-  const int ngroups = (1 << logC) << __popc((uint32_t)gm[kGmPass]);
+  static_assert(U <= 4, "head group slots");
+  const int ngroups = (1 << logC) << __popc((uint32_t)h.w[kS2PmPass]);
   const int cmb = ((1 << logC) - 1) << SH;
   int ka[K], na[N];   // byte offsets (the LUT entries are staged as byte offsets too)
 #pragma unroll
-  for (int k = 0; k < K; ++k) ka[k] = gm[kGmKaddr + k] << SH;
+  for (int k = 0; k < K; ++k) ka[k] = h.w[kS2PmAddr + k] << SH;
 #pragma unroll
-  for (int n = 0; n < N; ++n) na[n] = gm[kGmNaddr + n] << SH;
+  for (int n = 0; n < N; ++n) na[n] = h.w[kS2PmCode + n] << SH;
   T creg[kReg ? K * N : 1];
   if constexpr (kReg) {
 #pragma unroll
@@ -362,18 +371,19 @@ __device__ __forceinline__ void blk_gate(T (&x)[1 << B], const T* cf, int code) 
 }
 
 template <typename T, int B>
-__device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restrict__ cf_all,
-                                           const int32_t* __restrict__ pm,
-                                           const int32_t* __restrict__ lut, int logC) {
+__device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restrict__ cf_all, const PassHead& h,
+                                           const int32_t* __restrict__ pml, const int32_t* __restrict__ lut,
+                                           int logC) {
   constexpr int E = 1 << B;
   constexpr int SH = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;
   char* const bb = reinterpret_cast<char*>(buf);
+  const int32_t* const pm = h.w;   // constant indices only (a register copy); codes from pml (LDS)
   const int ngroups = (1 << logC) << __popc((uint32_t)pm[kS2PmPass]);
   const int cmb = ((1 << logC) - 1) << SH;
   // block-bit address parts are wave-uniform: scalar registers, element offsets formed by SALU
   int ba[B];
 #pragma unroll
-  for (int b = 0; b < B; ++b) ba[b] = __builtin_amdgcn_readfirstlane(pm[kS2PmAddr + b] << SH);
+  for (int b = 0; b < B; ++b) ba[b] = pm[kS2PmAddr + b] << SH;
   auto off = [&](int e) {
     int o = 0;
 #pragma unroll
@@ -390,18 +400,17 @@ __device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restr
     for (int e = 0; e < E; ++e) x[e] = *reinterpret_cast<const T*>(bb + (a0 ^ off(e)));
     // the element addresses are recomputed for the write-back (not held across the gates)
     asm volatile("" : "+v"(a0));
-    for (int q = 0; q < cnt; ++q) blk_gate<T, B>(x, cf_all + (first + q) * kCf, pm[kS2PmCode + q]);
+    for (int q = 0; q < cnt; ++q) blk_gate<T, B>(x, cf_all + (first + q) * kCf, pml[kS2PmCode + q]);
 #pragma unroll
     for (int e = 0; e < E; ++e) *reinterpret_cast<T*>(bb + (a0 ^ off(e))) = x[e];
   }
 }
 
 template <typename T>
-__device__ __forceinline__ void run_gate(T* buf, const T* cf, const int32_t* gm, const int32_t* lut,
-                                         int logC) {
+__device__ __forceinline__ void run_gate(T* buf, const T* cf, const PassHead& h, const int32_t* lut, int logC) {
 #define TQ_GATE(k, n) \
-  case k * 16 + n: gate_pass<T, k, n>(buf, cf, gm, lut, logC); break;
-  switch (gm[kGmK] * 16 + gm[kGmN]) {
+  case k * 16 + n: gate_pass<T, k, n>(buf, cf, h, lut, logC); break;
+  switch (h.w[kS2PmCount] >> 8) {   // K * 16 + N
     TQ_GATE(1, 1) TQ_GATE(1, 2) TQ_GATE(1, 4) TQ_GATE(1, 8)
     TQ_GATE(2, 1) TQ_GATE(2, 2) TQ_GATE(2, 4) TQ_GATE(2, 8)
     TQ_GATE(4, 1) TQ_GATE(4, 2) TQ_GATE(4, 4) TQ_GATE(4, 8)
@@ -680,6 +689,13 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     else TQ_BY_COUNT(RMAX, rin, t[r] = *lane_at(Xr + uniform(base + keep.ld_hm[r]), ldo));
     TQ_BY_COUNT(RMAX, rin, bufr[lda ^ keep.ld_ha[r]] = t[r]);
   };
+  // a pass's head (PassHead): the pmeta row, one batch of LDS reads into scalar registers (the
+  // pass's group-table reads do not depend on it: rows by pass)
+  auto read_head = [&](int p, PassHead& h) {
+    const int32_t* const pm = pmeta + p * 16;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) h.w[i] = __builtin_amdgcn_readfirstlane(pm[i]);
+  };
   Raw reg0[RMAX];
   // ---- a cooperative op waits for every workgroup's arrival after the previous ops (their
   // stores complete): one lane polls the counter, the others wait at the barrier.  Every
@@ -739,20 +755,22 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     const bool more = nxt < nchunks;
     if (more) prefetch(i + 1, nxt);
     for (int p = 0; p < npass; ++p) {
-      const int32_t* pm = pmeta + p * 16;
-      const int g = pm[kS2PmFirst];
-      const int bk = pm[kS2PmB];
-      if (bk == 0) run_gate<T>(buf, cf + g * kCf, gmeta + g * kGm, lut + g * kLut, logC);
+      PassHead cur;
+      read_head(p, cur);
+      const int g = cur.w[kS2PmFirst];
+      const int bk = cur.w[kS2PmB];
+      const int32_t* const lp = lut + p * kLut;   // the pass's group table (rows by pass)
+      if (bk == 0) run_gate<T>(buf, cf + g * kCf, cur, lp, logC);
       else if (bk == 4) {
-        if constexpr (sizeof(T) <= 8) block_pass<T, 4>(buf, cf, pm, lut + g * kLut, logC);
+        if constexpr (sizeof(T) <= 8) block_pass<T, 4>(buf, cf, cur, pmeta + p * 16, lp, logC);
       }
-      else block_pass<T, 3>(buf, cf, pm, lut + g * kLut, logC);
+      else block_pass<T, 3>(buf, cf, cur, pmeta + p * 16, lp, logC);
       __syncthreads();
 #ifdef TQ_S2_TIMING
       if (ch == lb && ts_rec && threadIdx.x == 0 && p < 16) {
         g_s2_ts[ts_idx][9 + p] = clock64() - clk0;
         g_s2_ts[ts_idx][25 + p] = ((unsigned long long)bk << 16) | (gmeta[g * kGm + kGmK] << 8) |
-                                  gmeta[g * kGm + kGmN] | ((unsigned long long)pm[kS2PmCount] << 24);
+                                  gmeta[g * kGm + kGmN] | ((unsigned long long)(cur.w[kS2PmCount] & 0xff) << 24);
       }
 #endif
     }
