@@ -1,11 +1,48 @@
 // extern "C" surface of libtneqhip.so (declared in include/tneqhip.h).
 #include <cstring>
+#include <string>
 #include <exception>
 #include <new>
 
 #include "tq_common.h"
 #include "tq_optim.h"
 #include "tq_plan.h"
+
+// development aid: TQ_TRACE_FILE=<path> appends a line per plan execute / destroy step (finds
+// which call a native abort comes from when the test runner swallows stderr)
+static void trace(const char* what, const void* p, int64_t v = 0) {
+  static const char* path = getenv("TQ_TRACE_FILE");
+  if (!path) return;
+  if (FILE* f = fopen(path, "a")) {
+    fprintf(f, "%s %p %lld\n", what, p, (long long)v);
+    fclose(f);
+  }
+}
+// ... and records the exception behind a std::terminate (an exception leaving a destructor)
+static const bool g_trace_terminate = [] {
+  if (!getenv("TQ_TRACE_FILE")) return false;
+  static std::terminate_handler prev = std::set_terminate([] {
+    const char* what = "(no exception)";
+    std::string msg;
+    if (auto ep = std::current_exception()) {
+      try {
+        std::rethrow_exception(ep);
+      } catch (const std::exception& e) {
+        msg = e.what();
+        what = msg.c_str();
+      } catch (...) {
+        what = "(non-std exception)";
+      }
+    }
+    if (FILE* f = fopen(getenv("TQ_TRACE_FILE"), "a")) {
+      fprintf(f, "terminate: %s\n", what);
+      fclose(f);
+    }
+    if (prev) prev();
+    abort();
+  });
+  return true;
+}();
 
 namespace tq {
 namespace {
@@ -286,8 +323,11 @@ int tq_plan_execute(tq_plan p, const void* const* inputs, void* out, int64_t sli
     TQ_TRY(tq::plan_materialize(p->plan, nullptr, nullptr, (hipStream_t)stream));
     p->materialized = true;
   }
-  return tq::plan_run(p->plan, inputs, out, slice_begin, slice_end, slice_step, accumulate,
-                      (hipStream_t)stream);
+  trace("execute", p, (int64_t)(intptr_t)stream);
+  const int rc = tq::plan_run(p->plan, inputs, out, slice_begin, slice_end, slice_step, accumulate,
+                              (hipStream_t)stream);
+  trace("executed", p, rc);
+  return rc;
   TQ_GUARD_END
 }
 
@@ -358,8 +398,11 @@ int tq_fidelity_backward(int dtype, int64_t n, const void* t, const void* o, con
 
 int tq_plan_destroy(tq_plan p) {
   if (!p) return TQ_OK;
+  trace("destroy", p, (int64_t)p->plan.graphs.size());
   tq::plan_release(p->plan);
+  trace("released", p);
   delete p;
+  trace("deleted", p);
   return TQ_OK;
 }
 

@@ -566,7 +566,8 @@ class _TreeRuntime:
             self.graphs.pop(next(iter(self.graphs)))
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.dev)
-        with torch.cuda.graph(g):
+        from .graphs import gc_paused   # (no collection inside the capture: graphs.gc_paused)
+        with gc_paused(), torch.cuda.graph(g):
             fn()
         self.graphs[key] = g
         g.replay()

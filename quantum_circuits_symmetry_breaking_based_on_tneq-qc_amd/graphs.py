@@ -12,9 +12,27 @@ retraction runs, exactly as in the reference.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from typing import Callable, Sequence, Tuple
 
 import torch
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """Python's cyclic GC off for the duration (wrap a whole ``torch.cuda.graph`` capture in it).
+    A collection triggered by an allocation inside a capture can run a finalizer that destroys
+    another CUDAGraph (hipGraphExecDestroy), which HIP refuses while a stream is capturing: the
+    refusal is raised inside ~CUDAGraph and terminates the process.  torch's capture context
+    still runs its explicit gc.collect() before the capture begins."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def capture_step(step_fn: Callable[[], torch.Tensor], params: Sequence[torch.Tensor],
@@ -36,7 +54,7 @@ def capture_step(step_fn: Callable[[], torch.Tensor], params: Sequence[torch.Ten
     for p in params:
         p.grad = None
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
+    with gc_paused(), torch.cuda.graph(g, stream=s):
         loss = step_fn()
     torch.cuda.synchronize(device)
     return g, loss

@@ -42,7 +42,7 @@ from tneq_qc_amd.circuits import BrickWall, TRAIN_MASK  # noqa: E402
 from tneq_qc_amd.contractor import EinsumStrategy  # noqa: E402
 from tneq_qc_amd.einsum import parse_equation, partition_path  # noqa: E402
 from tneq_qc_amd.expression import HipContractExpression  # noqa: E402
-from tneq_qc_amd.graphs import capture_step  # noqa: E402
+from tneq_qc_amd.graphs import capture_step, gc_paused  # noqa: E402
 from tneq_qc_amd.optim import SGDG  # noqa: E402
 
 N_Q, DEPTH = 8, 10
@@ -141,7 +141,7 @@ def capture_all(target, cands, dev, warmup=2):
     for p in allp:
         p.grad = None
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=cap):
+    with gc_paused(), torch.cuda.graph(g, stream=cap):
         losses = run_all()
     torch.cuda.synchronize(dev)
     return g, losses
