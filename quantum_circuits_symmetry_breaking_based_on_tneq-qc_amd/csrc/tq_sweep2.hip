@@ -210,10 +210,9 @@ struct PassHead {
 // group (lut[pp] ^ c) ^ input k (kaddr[k]) / output n (naddr[n]).  U groups per thread in
 // flight; all K inputs of a group are read before any of its N outputs is written (outputs
 // reuse the input positions).
-template <typename T, int K, int N>
-__device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restrict__ cf, const PassHead& h,
-                                          const int32_t* __restrict__ lut, int logC) {
-  constexpr int U = sizeof(T) > 8 ? (K * N >= 8 ? 1 : 2) : (K * N >= 16 ? 2 : 4);
+template <typename T, int K, int N, int U>
+__device__ __forceinline__ void gate_pass_u(T* __restrict__ buf, const T* __restrict__ cf, const PassHead& h,
+                                            const int32_t* __restrict__ lut, int logC) {
   // coefficients held in registers (up to 32 VGPRs for FP32 data, 16 for FP64); larger gates
   // re-read them from LDS per group
   constexpr bool kReg = K * N * sizeof(T) <= (sizeof(typename Traits<T>::R) == 4 ? 128 : 64);
@@ -272,6 +271,31 @@ __device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restri
       }
     }
   }
+}
+
+// U groups per thread in flight; a chunk of at most one group per thread (the small tiles: C2's
+// 2048-element chunks under a 4x4 gate, 512 groups) runs the one-group form -- the U-wide one
+// computed U - 1 duplicate groups there, half or more of the pass's VALU (r04 probe,
+// probes/pass_probe.hip: a 4x4 pass over 2048 elements is VALU-issue bound at ~1000 clocks with
+// one group per thread)
+template <typename T, int K, int N>
+__device__ __forceinline__ void gate_pass(T* __restrict__ buf, const T* __restrict__ cf, const PassHead& h,
+                                          const int32_t* __restrict__ lut, int logC) {
+  constexpr int U = sizeof(T) > 8 ? (K * N >= 8 ? 1 : 2) : (K * N >= 16 ? 2 : 4);
+  if constexpr (U > 1) {
+    const int ngroups = (1 << logC) << __popc((uint32_t)h.w[kS2PmPass]);
+    if (ngroups <= NT) {
+      gate_pass_u<T, K, N, 1>(buf, cf, h, lut, logC);
+      return;
+    }
+    if constexpr (U > 2) {
+      if (ngroups <= 2 * NT) {
+        gate_pass_u<T, K, N, 2>(buf, cf, h, lut, logC);
+        return;
+      }
+    }
+  }
+  gate_pass_u<T, K, N, U>(buf, cf, h, lut, logC);
 }
 
 // ---- register blocks (S2Desc::pmeta): a run of square gates applied to 2^B elements per group
