@@ -1178,6 +1178,18 @@ class Compiler {
     }();
     return v;
   }
+  // ... for tiles of >= 2^9 positions (TQ_S2_MINLC_BIG, default 0: one column): such a chunk
+  // holds >= 512 elements per column, so a narrower chunk halves a workgroup's gate-pass VALU
+  // (passes are VALU-issue bound, probes/pass_probe.hip) and doubles the workgroups.  Measured
+  // r04 (C2: 26 levels of 1024-position tiles, 2 -> 1 column, 4 -> 8 chunks): 0.323 -> 0.303 ms;
+  // applied to every small tensor it left C3 / the C4 N = 8 rank +-0.4 % (not kept there)
+  static int s2_min_logc_big() {
+    static const int v = [] {
+      const char* e = getenv("TQ_S2_MINLC_BIG");
+      return e ? std::max(0, std::min(5, atoi(e))) : 0;
+    }();
+    return v;
+  }
   // narrowest chunk (log2 columns) of a sweep2 op before the tile / min-chunk caps (TQ_S2_LC):
   // 7 since r03 (C3's per-slice ops, 128-element tiles: 32 -> 128 columns per chunk, 1.16 ->
   // 1.04 ms per step with the capped launches; C4 and C2 +-0; 8-10 no better)
@@ -1420,7 +1432,8 @@ class Compiler {
         mc > 1) {
       int lg = 0;
       while ((2 << lg) <= mc) ++lg;
-      lc = std::min(lc, std::max(std::min(s2_min_logc(), d.colbits), d.colbits - lg));
+      const int minlc = used >= 9 ? std::min(s2_min_logc(), s2_min_logc_big()) : s2_min_logc();
+      lc = std::min(lc, std::max(std::min(minlc, d.colbits), d.colbits - lg));
     }
     if (one_chunk_) lc = std::min(lc_cap, d.colbits);   // the chain-launch form (Op::stab1)
     d.logC = lc;

@@ -76,8 +76,7 @@ def test_chain_launch_equals_one_launch_per_level(dev, cfg):
 
 def test_cooperative_chain_equals_one_launch_per_level(dev):
     """C2's 26 levels of one multi-chunk sweep2 op run as ONE cooperative launch with
-    "sweep_coop" = 1 (complex64: 4 workgroups; complex128, twice the chunks: 8 workgroups, 32 + 2
-    ops), each op's chunks spread over them, a counter barrier between the ops, sc1 loads /
+    "sweep_coop" = 1 (8 workgroups; complex128: 32 + 2 ops), each op's chunks spread over them, a counter barrier between the ops, sc1 loads /
     stores: tq_plan.cpp Plan::coop_once, S2Launch::sync); "sweep_coop" = 0 (the default, measured
     faster) launches them level by level.  Same descriptors, same arithmetic: the results are bit-identical, on every one of many
     graph replays (a missed barrier shows up as a stale chunk), eager and captured, and no wait
