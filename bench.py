@@ -427,7 +427,7 @@ def main():
     achieved = exe_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     alg_rate = alg_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     if f16:
-        pmc_b = _profile_json("pmc_gemm_f16_r04d.json" if f16_g3 else "pmc_gemm_f16_r02.json", args.config)
+        pmc_b = _profile_json("pmc_gemm_f16_r04g.json" if f16_g3 else "pmc_gemm_f16_r02.json", args.config)
         pmc_t = pmc_b
         kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_f16: every f32 operand scaled by a power of two "
                  "(operand max from its producer sweep) and split into 2 f16 terms, 3 term products kept, f32 "
