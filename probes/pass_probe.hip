@@ -7,6 +7,8 @@
 //   variant 3: variant 2 preceded by a dependent LDS read of the pass's metadata (the address
 //              base), i.e. two LDS round trips per pass
 //   variant 4: variant 2 with 4 groups per thread (8192-element tile instead of 2048)
+//   variant 5: a 4x4 gate on a 1024-element tile: 256 groups, threads >= 256 idle
+//   variant 6: the same with two threads per group (adjacent lanes), each computing 2 outputs
 // Usage: ./pass_probe  -> one JSON line per (variant, workgroups per CU)
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -30,6 +32,29 @@ __global__ void __launch_bounds__(NT) probe(unsigned long long* out, int salt) {
   for (int p = 0; p < P; ++p) {
     if constexpr (V == 1) {
       m = meta[(m + tid + p) & 63];
+    } else if constexpr (V == 5 || V == 6) {
+      // 1024-element tile: inputs at stride 256 (positions 8, 9)
+      const int grp = V == 5 ? tid : tid >> 1;
+      if (grp < 256) {
+        const int a = grp;
+        c64 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = tile[a + k * 256];
+        constexpr int NO = V == 5 ? 4 : 2;
+        const int n0 = V == 5 ? 0 : (tid & 1) * 2;
+#pragma unroll
+        for (int q = 0; q < NO; ++q) {
+          const int n = n0 + q;
+          c64 acc{0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const c64 cc = c[(k + n) & 3];
+            acc.re += x[k].re * cc.re - x[k].im * cc.im;
+            acc.im += x[k].re * cc.im + x[k].im * cc.re;
+          }
+          tile[a + n * 256] = acc;
+        }
+      }
     } else if constexpr (V >= 2) {
       int base = 0;
       if constexpr (V == 3) base = meta[(m + p) & 63] & 1;   // the pass's metadata first
@@ -90,6 +115,8 @@ int main() {
     run<2>(wgs, d, "4x4 gate, 1 group per thread");
     run<3>(wgs, d, "metadata read + 4x4 gate");
     run<4>(wgs, d, "4x4 gate, 4 groups per thread");
+    run<5>(wgs, d, "4x4 gate on 1024 elements, 256 threads");
+    run<6>(wgs, d, "4x4 gate on 1024 elements, 2 threads per group");
   }
   hipFree(d);
   return 0;
