@@ -9,6 +9,8 @@
 //   variant 4: variant 2 with 4 groups per thread (8192-element tile instead of 2048)
 //   variant 5: a 4x4 gate on a 1024-element tile: 256 groups, threads >= 256 idle
 //   variant 6: the same with two threads per group (adjacent lanes), each computing 2 outputs
+//   variant 7: variant 5 with the 16 coefficients read from LDS every pass (broadcast reads)
+//   variant 8: variant 7 with the coefficients made wave-uniform (readfirstlane: scalar registers)
 // Usage: ./pass_probe  -> one JSON line per (variant, workgroups per CU)
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -32,6 +34,36 @@ __global__ void __launch_bounds__(NT) probe(unsigned long long* out, int salt) {
   for (int p = 0; p < P; ++p) {
     if constexpr (V == 1) {
       m = meta[(m + tid + p) & 63];
+    } else if constexpr (V == 7 || V == 8) {
+      __shared__ c64 cfl[16];
+      if (p == 0 && tid < 16) cfl[tid] = c64{0.1f * tid, 0.05f * tid};
+      if (p == 0) __syncthreads();
+      c64 cc[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        cc[i] = cfl[(i + m) & 15];
+        if constexpr (V == 8) {
+          cc[i].re = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc[i].re)));
+          cc[i].im = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc[i].im)));
+        }
+      }
+      const int grp = tid;
+      if (grp < 256) {
+        const int a = grp;
+        c64 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = tile[a + k * 256];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          c64 acc{0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            acc.re += x[k].re * cc[k * 4 + n].re - x[k].im * cc[k * 4 + n].im;
+            acc.im += x[k].re * cc[k * 4 + n].im + x[k].im * cc[k * 4 + n].re;
+          }
+          tile[a + n * 256] = acc;
+        }
+      }
     } else if constexpr (V == 5 || V == 6) {
       // 1024-element tile: inputs at stride 256 (positions 8, 9)
       const int grp = V == 5 ? tid : tid >> 1;
@@ -117,6 +149,8 @@ int main() {
     run<4>(wgs, d, "4x4 gate, 4 groups per thread");
     run<5>(wgs, d, "4x4 gate on 1024 elements, 256 threads");
     run<6>(wgs, d, "4x4 gate on 1024 elements, 2 threads per group");
+    run<7>(wgs, d, "variant 5 + coefficients from LDS each pass");
+    run<8>(wgs, d, "variant 7 with scalar (readfirstlane) coefficients");
   }
   hipFree(d);
   return 0;
