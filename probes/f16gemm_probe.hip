@@ -1,0 +1,272 @@
+// f16 GEMM probe (r05): what a plain f16 MFMA GEMM with LDS-DMA staging reaches on the boundary
+// GEMM's shape when the f32 -> f16 term split is done by the operand's producer instead of inside
+// the GEMM.  The production kernel (tq_gemm.hip, gemm_c64_kouter_split_kernel) executes
+// 18 M N K f16 MFMA flops per 4-lane launch (Gauss 3M x 3 term products) at ~0.95 PF; the same
+// flops as plain GEMMs are 12 batch entries (4 lanes x 3 real products) of
+// M = N = 1024, K' = 3 x 65536 (the three term products concatenated along K).
+//
+//   C[b][m][n] = sum_k A[b][k][m] B[b][k][n]     (f16 in, f32 accumulate, K-outer operands)
+//
+// Tile 256 x 256 x 64 per 512-thread workgroup, 8 waves (2 over M x 4 over N) of 128 x 64 on
+// v_mfma_f32_16x16x32_f16, operands [k][m] / [k][n] staged by global_load_lds_dwordx4 into an
+// XOR-swizzled image (32-B chunk index ^ f(k)) read by ds_read_b64_tr_b16 (conflict-free), split-K
+// to fill the chip, XCD-aware workgroup order (a (batch, split) group of 16 tiles on one XCD).
+// Usage: ./f16gemm_probe [variant ...]  -> one JSON line per variant.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));        \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define LDS __attribute__((address_space(3)))
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int TB = BK * BM * 2;  // bytes of one operand tile (32 KiB)
+
+struct Args {
+  const _Float16* A;
+  const _Float16* B;
+  float* C;  // [batch][split][M][N] partials
+  int M, N, batch, splits;
+  long long K, kchunk;
+  unsigned long long* stamps;  // [wg][4]: memtime, memrealtime at loop start / end (VAR & 16)
+};
+
+// deterministic operand values: uniform in [-1, 1) as f16
+__host__ __device__ inline float hval(uint64_t i, uint32_t salt) {
+  uint64_t x = i * 0x9E3779B97F4A7C15ull + salt;
+  x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29; x *= 0x94D049BB133111EBull; x ^= x >> 32;
+  return ((float)(x & 0xffffff) / 8388608.f) - 1.f;
+}
+__global__ void fill(_Float16* p, uint64_t n, uint32_t salt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (_Float16)hval(i, salt);
+}
+
+__device__ __forceinline__ int fsw(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+template <int VAR>
+__global__ void __launch_bounds__(NT) gemm(Args g) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int nt = g.N / BN, ntile = (g.M / BM) * nt;
+  const int tile = L % ntile, grp = L / ntile;
+  const int split = grp % g.splits, b = grp / g.splits;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
+  const long long k0 = split * g.kchunk;
+  const int nk = (int)(g.kchunk / BK);
+  const _Float16* Ab = g.A + ((long long)b * g.K + k0) * g.M + m0;
+  const _Float16* Bb = g.B + ((long long)b * g.K + k0) * g.N + n0;
+
+  // LDS-DMA: wave-instruction i of wave w fills LDS bytes [(8 i + w) KiB, +1 KiB) = tile rows
+  // 2 (8 i + w) and + 1; lane l: row r, 32-B chunk c' = (l & 31) >> 1, half l & 1, which holds
+  // the global chunk c' ^ f(r)
+  uint32_t goA[4], goB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 2 * (8 * i + w) + (lane >> 5);
+    const int c = ((lane & 31) >> 1) ^ fsw(r);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8);
+    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8);
+  }
+  // the DMA is issued from inline asm: hipcc would treat an in-flight LDS-DMA as a possible alias
+  // of the next ds_read and drain it with vmcnt(0); the waits are placed by hand
+  const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
+  auto glds16 = [&](const void* src, unsigned off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  auto stage = [&](int t, int buf) {
+    const _Float16* pa = Ab + (long long)t * BK * g.M;
+    const _Float16* pb = Bb + (long long)t * BK * g.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(pa + goA[i], buf * 2 * TB + (8 * i + w) * 1024);
+      glds16(pb + goB[i], buf * 2 * TB + TB + (8 * i + w) * 1024);
+    }
+  };
+
+  // transposed fragment reads: lane l = 16 g4 + 4 q + p reads row k = 32 kk + 8 g4 + 4 u + q,
+  // 8 B at columns 4p .. 4p+3 of chunk (16-column group) c, stored at chunk c ^ f(k), f(k) = x
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int x = q | ((g4 & 1) << 2);
+  const int rowb = (8 * g4 + q) * (BM * 2) + 8 * p;
+  int aoff[8], boff[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) aoff[i] = rowb + ((wm * 8 + i) ^ x) * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) boff[j] = TB + rowb + ((wn * 4 + j) ^ x) * 32;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto rd = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BM * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+  };
+
+  unsigned long long t0 = 0, r0 = 0;
+  if constexpr (VAR & 16) {
+    if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  }
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const char* s = lds + (t & 1) * 2 * TB;
+    if (t + 1 < nk) stage(t + 1, (t & 1) ^ 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f16x8 fa[8], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = rd(s, boff[j] + kk * 32 * BM * 2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = rd(s, aoff[i] + kk * 32 * BM * 2);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if constexpr (VAR & 16) {
+    if (tid == 0) {
+      unsigned long long* st = g.stamps + 4 * blockIdx.x;
+      st[0] = t0; st[1] = r0; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + i * 16 + g4 * 4 + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        C[(long long)m * g.N + n] = acc[i][j][r];
+      }
+}
+
+template <int VAR>
+static void run(const char* name, Args g, int nwg, bool check) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  // warm the clock: ~2 s of back-to-back launches
+  CK(hipEventRecord(e0));
+  int nw = 0;
+  for (;;) {
+    hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+    ++nw;
+    if (nw % 20 == 0) {
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms > 2000.f || nw >= 400) break;
+    }
+  }
+  const int R = 10;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < R; ++r) hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= R;
+  const double fl = 2.0 * g.M * g.N * (double)g.K * g.batch;
+  double clk = 0;
+  if (VAR & 16) {
+    std::vector<unsigned long long> st(4 * (size_t)nwg);
+    CK(hipMemcpy(st.data(), g.stamps, st.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> c;
+    for (int i = 0; i < nwg; ++i) {
+      const double dt = (double)(st[4 * i + 2] - st[4 * i]), dr = (double)(st[4 * i + 3] - st[4 * i + 1]);
+      if (dr > 0) c.push_back(dt / dr * 100.0);  // MHz
+    }
+    std::sort(c.begin(), c.end());
+    if (!c.empty()) clk = c[c.size() / 2];
+  }
+  double maxrel = -1;
+  if (check) {
+    // 24 sampled outputs against an f64 host dot product of the same operand values
+    std::vector<float> part((size_t)g.splits);
+    maxrel = 0;
+    for (int s = 0; s < 24; ++s) {
+      const int b = (s * 7) % g.batch, m = (s * 389 + 11) % g.M, n = (s * 613 + 5) % g.N;
+      double ref = 0, nrm = 0;
+      for (long long k = 0; k < g.K; ++k) {
+        const double a = (double)(_Float16)hval(((uint64_t)b * g.K + k) * g.M + m, 1);
+        const double bb = (double)(_Float16)hval(((uint64_t)b * g.K + k) * g.N + n, 2);
+        ref += a * bb;
+        nrm += fabs(a * bb);
+      }
+      double got = 0;
+      for (int sp = 0; sp < g.splits; ++sp) {
+        float v;
+        CK(hipMemcpy(&v, g.C + (((size_t)(b * g.splits + sp) * g.M + m) * g.N + n), 4, hipMemcpyDeviceToHost));
+        got += v;
+      }
+      maxrel = std::max(maxrel, fabs(got - ref) / nrm);
+    }
+  }
+  printf("{\"variant\": \"%s\", \"ms\": %.4f, \"tflops\": %.1f, \"frac_f16_peak\": %.4f, \"clock_mhz\": %.0f, "
+         "\"warm_launches\": %d, \"check_max_err_rel_sum_abs\": %.3e}\n",
+         name, ms, fl / ms / 1e9, fl / ms / 1e9 / 2500.0, clk, nw, maxrel);
+  fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+  Args g{};
+  g.M = g.N = 1024;
+  g.batch = 12;
+  g.K = 3 * 65536;
+  g.splits = 4;
+  g.kchunk = g.K / g.splits;
+  const int nwg = g.batch * g.splits * (g.M / BM) * (g.N / BN);
+  const size_t na = (size_t)g.batch * g.K * g.M, nb = (size_t)g.batch * g.K * g.N;
+  _Float16 *A, *B;
+  CK(hipMalloc(&A, na * 2));
+  CK(hipMalloc(&B, nb * 2));
+  CK(hipMalloc(&g.C, (size_t)g.batch * g.splits * g.M * g.N * 4));
+  CK(hipMalloc(&g.stamps, (size_t)nwg * 4 * 8));
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, A, (uint64_t)na, 1u);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, B, (uint64_t)nb, 2u);
+  CK(hipDeviceSynchronize());
+  g.A = A;
+  g.B = B;
+  int v = argc > 1 ? atoi(argv[1]) : 0;
+  if (v == 0 || v == 1) run<0>("base", g, nwg, true);
+  if (v == 0 || v == 2) run<1>("setprio", g, nwg, false);
+  if (v == 0 || v == 3) run<16>("base_stamps", g, nwg, false);
+  return 0;
+}

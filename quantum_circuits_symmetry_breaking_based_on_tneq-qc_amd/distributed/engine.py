@@ -46,6 +46,7 @@ import torch.distributed as dist
 
 from ..contractor.greedy_symbolic import greedy_equation
 from ..core.tn_tensor import TNTensor
+from .comm import comm_group, comm_rank_size, get_comm_backend
 from .tree import TreeContraction
 
 
@@ -110,18 +111,19 @@ class DistributedEngineSiamese:
                  partition_config: Optional[PartitionConfig] = None, comm_timeout: float = 300.0,
                  enable_comm_retry: bool = True, max_comm_retries: int = 3,
                  executor: Optional[Callable] = None):
-        """`comm`: the torch.distributed process group the engine runs on (None = WORLD; the
-        reference's CommBase is torch.distributed here).  `executor` is passed to TreeContraction
-        (None = the native plan; CPU tests inject a torch executor)."""
+        """`comm`: the reference's communicator (`distributed.comm.CommTorch` / `MockCommTorch`,
+        as `get_comm_backend('torch' | 'mock' | 'auto')` builds it for `distributed_trainer.py:228-233`)
+        or a torch.distributed process group; None = `get_comm_backend('auto')` (WORLD when a group
+        is initialised, else a 1-rank mock) as the reference's `comm or get_comm_backend(...)`
+        (`:248`).  Collectives run on the communicator's group.  `executor` is passed to
+        TreeContraction (None = the native plan; CPU tests inject a torch executor)."""
         self._backend_arg = backend
         self.strategy_mode = strategy_mode
         self.mx_K = mx_K
         self._base = None
-        self.group = comm
-        self.comm = comm
-        on = dist.is_available() and dist.is_initialized()
-        self.rank = dist.get_rank(comm) if on else 0
-        self.world_size = dist.get_world_size(comm) if on else 1
+        self.comm = comm if comm is not None else get_comm_backend("auto")
+        self.group = comm_group(self.comm)
+        self.rank, self.world_size = comm_rank_size(self.comm)
         self.comm_timeout = comm_timeout
         self.enable_comm_retry = enable_comm_retry
         self.max_comm_retries = max_comm_retries
