@@ -146,7 +146,9 @@ int64_t tq_plan_query(tq_plan plan, const char* key);
  * 0 launches them eagerly on the stream (use when the caller captures the stream itself);
  * "sweep_chain" = 1 (default, env TQ_S2_SEQ) runs consecutive hoisted levels that are each one
  * small sweep2 op as one launch of one workgroup (query "n_chain_launches"), 0 one launch per
- * level. */
+ * level; "sweep_coop" = 0 (default, env TQ_S2_COOP) -- 1 runs consecutive hoisted levels of
+ * multi-chunk sweep2 ops as one launch whose workgroups hand off through a counter barrier
+ * (diagnostic: measured slower; a wait that gives up is counted in query "coop_timeouts"). */
 int tq_plan_set(tq_plan plan, const char* key, int64_t value);
 /* human-readable per-step description into buf (for debugging / DESIGN evidence) */
 int tq_plan_describe(tq_plan plan, char* buf, size_t n);
@@ -155,6 +157,10 @@ int tq_plan_describe(tq_plan plan, char* buf, size_t n);
  * (out = sum + (accumulate ? out : 0)).  inputs[i] are device pointers of the FULL inputs.  */
 int tq_plan_execute(tq_plan plan, const void* const* inputs, void* out, int64_t slice_begin,
                     int64_t slice_end, int64_t slice_step, int accumulate, void* stream);
+/* Releases the plan's graphs, events, streams and device memory.  TQ_ERR_HIP when HIP refuses a
+ * release (e.g. hipGraphExecDestroy / hipFree while a stream capture is in progress in this
+ * process): the plan stays valid with whatever it still holds, and a later tq_plan_destroy
+ * retries; nothing is released twice.  */
 int tq_plan_destroy(tq_plan plan);
 
 /* Per-op timing with HIP events recorded on the execution stream around every kernel of the

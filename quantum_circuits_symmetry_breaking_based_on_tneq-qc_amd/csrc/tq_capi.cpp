@@ -399,8 +399,12 @@ int tq_fidelity_backward(int dtype, int64_t n, const void* t, const void* o, con
 int tq_plan_destroy(tq_plan p) {
   if (!p) return TQ_OK;
   trace("destroy", p, (int64_t)p->plan.graphs.size());
-  tq::plan_release(p->plan);
-  trace("released", p);
+  // a refused release (e.g. a stream capture in progress elsewhere in the process) keeps the
+  // plan and what it still holds: the caller retries the destroy later (the Python host defers
+  // it until no capture is in progress); nothing is leaked or released twice
+  const int rc = tq::plan_release(p->plan);
+  trace("released", p, rc);
+  if (rc != TQ_OK) return rc;
   delete p;
   trace("deleted", p);
   return TQ_OK;

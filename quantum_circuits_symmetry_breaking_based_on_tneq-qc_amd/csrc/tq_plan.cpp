@@ -2371,35 +2371,63 @@ bool graphs_disabled() {
 bool graphs_enabled() { return !graphs_disabled(); }
 namespace {
 
-void drop_graph_entry(Plan::GraphEntry& g) {
-  if (g.done) { (void)hipEventSynchronize(g.done); (void)hipEventDestroy(g.done); }
-  if (g.exec) (void)hipGraphExecDestroy(g.exec);
-  if (g.graph) (void)hipGraphDestroy(g.graph);
-  g = Plan::GraphEntry{};
+// HIP release calls: the first failure is recorded (tq_last_error) and reported; a resource is
+// forgotten only once its release succeeded, so a release refused mid-way (e.g. by a stream
+// capture elsewhere in the process: HIP refuses hipGraphExecDestroy / hipFree while any stream
+// captures in global mode) can be retried later with nothing leaked or freed twice
+int rel(hipError_t e, const char* what, int& rc) {
+  if (e == hipSuccess) return 1;
+  if (rc == TQ_OK) set_error(std::string("HIP error ") + hipGetErrorString(e) + " releasing " + what);
+  rc = TQ_ERR_HIP;
+  return 0;
 }
 
-void drop_graph(Plan& P) {
-  for (auto& g : P.graphs) drop_graph_entry(g);
-  P.graphs.clear();
+int drop_graph_entry(Plan::GraphEntry& g) {
+  int rc = TQ_OK;
+  if (g.done && rel(hipEventSynchronize(g.done), "graph event", rc) && rel(hipEventDestroy(g.done), "graph event", rc))
+    g.done = nullptr;
+  if (g.exec && rel(hipGraphExecDestroy(g.exec), "graph exec", rc)) g.exec = nullptr;
+  if (g.graph && rel(hipGraphDestroy(g.graph), "graph", rc)) g.graph = nullptr;
+  if (rc == TQ_OK) g = Plan::GraphEntry{};
+  return rc;
+}
+
+int drop_graph(Plan& P) {
+  int rc = TQ_OK;
+  std::vector<Plan::GraphEntry> keep;
+  for (auto& g : P.graphs)
+    if (drop_graph_entry(g) != TQ_OK) {
+      rc = TQ_ERR_HIP;
+      keep.push_back(g);
+    }
+  P.graphs.swap(keep);
+  return rc;
 }
 
 }  // namespace
 
-void plan_release(Plan& P) {
-  drop_graph(P);
-  if (P.cap_stream) (void)hipStreamDestroy(P.cap_stream);
-  P.cap_stream = nullptr;
-  for (auto& ev : P.ev_used) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
-  for (auto& ev : P.ev_free) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
-  P.ev_used.clear();
-  P.ev_free.clear();
+int plan_release(Plan& P) {
+  int rc = drop_graph(P);
+  if (P.cap_stream && rel(hipStreamDestroy(P.cap_stream), "capture stream", rc)) P.cap_stream = nullptr;
+  auto drop_events = [&](std::vector<Plan::Ev>& v) {
+    std::vector<Plan::Ev> keep;
+    for (auto& ev : v) {
+      if (ev.a && rel(hipEventDestroy(ev.a), "event", rc)) ev.a = nullptr;
+      if (ev.b && rel(hipEventDestroy(ev.b), "event", rc)) ev.b = nullptr;
+      if (ev.a || ev.b) keep.push_back(ev);
+    }
+    v.swap(keep);
+  };
+  drop_events(P.ev_used);
+  drop_events(P.ev_free);
   if (P.owns_device) {
-    if (P.d_arena) (void)hipFree(P.d_arena);
-    if (P.d_tables) (void)hipFree(P.d_tables);
+    if (P.d_arena && rel(hipFree(P.d_arena), "arena", rc)) P.d_arena = nullptr;
+    if (P.d_tables && rel(hipFree(P.d_tables), "tables", rc)) P.d_tables = nullptr;
+  } else {
+    P.d_arena = P.d_tables = nullptr;
   }
-  P.d_arena = P.d_tables = nullptr;
-  if (P.h_bad) (void)hipHostFree(P.h_bad);
-  P.h_bad = nullptr;
+  if (P.h_bad && rel(hipHostFree(P.h_bad), "host flag", rc)) P.h_bad = nullptr;
+  return rc;
 }
 
 

@@ -181,7 +181,7 @@ struct Plan {
   std::vector<std::pair<int, int>> coop_once;
   std::vector<int> coop_width;
   size_t sync_off = 0;
-  bool use_coop = true;
+  bool use_coop = false;     // TQ_S2_COOP (default off) / tq_plan_set "sweep_coop"
   std::string describe;
   // hipGraph of the whole launch sequence of one execute call, replayed while the call's
   // pointers / slice range / flags are unchanged (a plan is hundreds of small launches)
@@ -192,7 +192,7 @@ struct Plan {
     int acc = 0;
     int mode = 0;   // Plan::run_mode the graph was captured with
     bool seq = true;  // Plan::use_seq
-    bool coop = true;  // Plan::use_coop
+    bool coop = false;  // Plan::use_coop
     bool operator==(const GraphKey& o) const {
       return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc &&
              mode == o.mode && seq == o.seq && coop == o.coop;
@@ -222,7 +222,7 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream);
 int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
              int64_t s_step, int accumulate, hipStream_t stream);
-void plan_release(Plan& P);
+int plan_release(Plan& P);   // TQ_OK, or TQ_ERR_HIP with what is left still held (retry later)
 int plan_profile_read(Plan& P, int kind, double* ms, int64_t* launches, double* flops, double* bytes);
 
 }  // namespace tq

@@ -224,7 +224,7 @@ class TreeContraction:
                 pos = r - st.g
                 H = 2 ** (st.s - 1)
                 members = [self.granks[q] for q in range(st.g, st.g + G)]
-                meta = _StageMeta(members, H, self.granks[r], self.group, st.shapes, cur.dtype, cur.device)
+                meta = _StageMeta(members, H, self.granks[r], self.group, st.shapes, cur.dtype, cur.device, tn)
                 # the left block (leader st.g) and the right block (leader st.g + H) to every
                 # member (the reference's SendRecvGrad exchange, distributed_engine.py:1697-1766),
                 # with their log-scales
@@ -264,11 +264,15 @@ def _exp(x: float) -> float:
 
 class _StageMeta:
     """Static description of one stage as seen by one member."""
-    __slots__ = ("members", "me", "group", "shapes", "dtype", "device", "H")
+    __slots__ = ("members", "me", "group", "shapes", "dtype", "device", "H", "scaled")
 
-    def __init__(self, members, H, me, group, shapes, dtype, device):
+    def __init__(self, members, H, me, group, shapes, dtype, device, scaled=True):
         self.members, self.H, self.me, self.group = members, H, me, group
         self.shapes, self.dtype, self.device = shapes, dtype, device
+        # log-scales travel with the blocks only when the call has TNTensor operands (every
+        # rank passes the same operand kinds); otherwise they are all 0: no extra messages and
+        # no host reads (.item()), so a plain distributed step stays asynchronous
+        self.scaled = scaled
 
     @property
     def leads(self):
@@ -340,18 +344,23 @@ def _exchange(cur, meta: _StageMeta, log_scale: float):
     for side, src in enumerate(leads):
         if me == src:
             payload = w.out(cur.contiguous())
-            ls = w.out(torch.tensor([log_scale], dtype=torch.float64, device=cur.device))
+            ls = w.out(torch.tensor([log_scale], dtype=torch.float64, device=cur.device)) if meta.scaled else None
             for m in mem:
                 if m != src:
-                    ops += [("send", payload, m), ("send", ls, m)]
+                    ops.append(("send", payload, m))
+                    if meta.scaled:
+                        ops.append(("send", ls, m))
         else:
             buf, dst = w.into(meta.shapes[side], meta.dtype, meta.device)
-            lbuf, ldst = w.into((1,), torch.float64, meta.device)
-            ops += [("recv", buf, src), ("recv", lbuf, src)]
+            ops.append(("recv", buf, src))
+            ldst = None
+            if meta.scaled:
+                lbuf, ldst = w.into((1,), torch.float64, meta.device)
+                ops.append(("recv", lbuf, src))
             got[side] = (dst, ldst)
     _p2p(ops, meta.group)
     w.finish()
-    return {side: (t, float(ls.item())) for side, (t, ls) in got.items()}
+    return {side: (t, float(ls.item()) if ls is not None else 0.0) for side, (t, ls) in got.items()}
 
 
 def _blocks(cur, rec: Dict[int, torch.Tensor], logs: Sequence[float]):
@@ -412,39 +421,49 @@ def _reduce(part, meta: _StageMeta, log_scale: float):
     if len(mem) == 1:
         return part, log_scale
     lead = mem[0]
+    sc = meta.scaled
     w = _Wire(meta.group)
-    ls_t = torch.tensor([log_scale], dtype=torch.float64, device=part.device)
     if me == lead:
         bufs, lbufs, ops = [], [], []
         for m in mem[1:]:
             buf, dst = w.into(tuple(part.shape), part.dtype, part.device)
-            lbuf, ldst = w.into((1,), torch.float64, part.device)
-            ops += [("recv", buf, m), ("recv", lbuf, m)]
+            ops.append(("recv", buf, m))
             bufs.append(dst)
-            lbufs.append(ldst)
+            if sc:
+                lbuf, ldst = w.into((1,), torch.float64, part.device)
+                ops.append(("recv", lbuf, m))
+                lbufs.append(ldst)
         _p2p(ops, meta.group)
         w.finish()
-        scales = [log_scale] + [float(l.item()) for l in lbufs]
+        scales = [log_scale] + ([float(l.item()) for l in lbufs] if sc else [0.0] * len(bufs))
         top = max(scales)
-        total = part * _exp_rel(scales[0], top)
+        total = part * _exp_rel(scales[0], top) if scales[0] != top else part
         for b, s in zip(bufs, scales[1:]):
-            total = total + b * _exp_rel(s, top)
+            total = total + (b * _exp_rel(s, top) if s != top else b)
         w2 = _Wire(meta.group)
         payload = w2.out(total.contiguous())
-        lt = w2.out(torch.tensor([top], dtype=torch.float64, device=part.device))
+        lt = w2.out(torch.tensor([top], dtype=torch.float64, device=part.device)) if sc else None
         ops = []
         for m in mem[1:]:
-            ops += [("send", payload, m), ("send", lt, m)]
+            ops.append(("send", payload, m))
+            if sc:
+                ops.append(("send", lt, m))
         _p2p(ops, meta.group)
         return total, top
-    ops = [("send", w.out(part.contiguous()), lead), ("send", w.out(ls_t), lead)]
+    ops = [("send", w.out(part.contiguous()), lead)]
+    if sc:
+        ops.append(("send", w.out(torch.tensor([log_scale], dtype=torch.float64, device=part.device)), lead))
     _p2p(ops, meta.group)
     w2 = _Wire(meta.group)
     buf, dst = w2.into(tuple(part.shape), part.dtype, part.device)
-    lbuf, ldst = w2.into((1,), torch.float64, part.device)
-    _p2p([("recv", buf, lead), ("recv", lbuf, lead)], meta.group)
+    rops = [("recv", buf, lead)]
+    ldst = None
+    if sc:
+        lbuf, ldst = w2.into((1,), torch.float64, part.device)
+        rops.append(("recv", lbuf, lead))
+    _p2p(rops, meta.group)
     w2.finish()
-    return dst, float(ldst.item())
+    return dst, (float(ldst.item()) if sc else 0.0)
 
 
 def _exp_rel(s: float, top: float) -> float:

@@ -21,7 +21,7 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
 
-from . import _lib
+from . import _lib, graphs
 from ._lib import check, i32, i64
 from .einsum import (Network, _State, greedy_path, linear_path, parse_equation, path_info,
                      validate_path)
@@ -36,6 +36,7 @@ class NativePlan:
     def __init__(self, net: Network, path: Sequence[Tuple[int, int]], dtype: torch.dtype,
                  strides: Optional[Sequence[Sequence[int]]], sliced: Sequence[int]):
         L = _lib.lib()
+        graphs.drain_deferred()
         ranks = [len(t) for t in net.terms]
         modes = [m for t in net.terms for m in t]
         exts = [net.extents[m] for t in net.terms for m in t]
@@ -58,7 +59,8 @@ class NativePlan:
     def set(self, key: str, value: int) -> None:
         """Plan option (tq_plan_set): "graph" (replay a captured hipGraph, default 1),
         "sweep_chain" (chain launches of small dependent sweep2 ops, default 1), "sweep_coop"
-        (cooperative launches of dependent multi-chunk sweep2 levels, default 1)."""
+        (cooperative launches of dependent multi-chunk sweep2 levels, default 0 = TQ_S2_COOP;
+        diagnostic, measured slower)."""
         check(_lib.lib().tq_plan_set(self._h, key.encode(), int(value)), "tq_plan_set")
 
     def describe(self) -> str:
@@ -76,6 +78,8 @@ class NativePlan:
                 end: Optional[int] = None, step: int = 1, accumulate: bool = False) -> None:
         """`ptrs`: the input base pointers (a sequence of ints, or an array from pointer_array)."""
         end = self.n_slices if end is None else end
+        if graphs._DEFERRED:
+            graphs.drain_deferred()
         arr = ptrs if isinstance(ptrs, ctypes.Array) else self.pointer_array(ptrs)
         rc = _lib.lib().tq_plan_execute(self._h, arr, ctypes.c_void_p(out_ptr), begin, end, step,
                                         int(accumulate), ctypes.c_void_p(stream))
@@ -103,14 +107,31 @@ class NativePlan:
                                               ctypes.byref(fl), ctypes.byref(by)), "tq_plan_profile_read")
         return {"ms": ms.value, "launches": n.value, "flops": fl.value, "bytes": by.value}
 
+    def release_now(self) -> None:
+        """Destroy the native plan; inside a stream capture (HIP refuses graph / memory releases
+        then) or when HIP refuses, the handle is parked and released after the capture
+        (graphs.drain_deferred)."""
+        h = getattr(self, "_h", None)
+        if h is None or _lib._lib is None:
+            return
+        if graphs.capturing() or _lib._lib.tq_plan_destroy(h) != 0:
+            graphs.defer_release(_PlanHandle(h))
+        self._h = None
+
     def __del__(self):
         try:
-            h = getattr(self, "_h", None)
-            if h is not None and _lib._lib is not None:
-                _lib._lib.tq_plan_destroy(h)
-                self._h = None
+            self.release_now()
         except Exception:  # interpreter shutdown: modules may already be gone
             pass
+
+
+class _PlanHandle:
+    """A native plan handle whose destroy was deferred (NativePlan.release_now)."""
+
+    def __init__(self, h):
+        self._h = h
+
+    release_now = NativePlan.release_now
 
 
 class HipContractExpression:
@@ -523,6 +544,17 @@ class _TreeRuntime:
         self.seen: Dict[tuple, int] = {}
         self.graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
 
+    def __del__(self):
+        # dropped inside a caller's capture: HIP would refuse the CUDAGraphs' destruction
+        # (hipGraphExecDestroy), so they are parked until the capture is over (the step plans
+        # park themselves, NativePlan.release_now)
+        try:
+            if getattr(self, "graphs", None) and graphs.capturing():
+                graphs.defer_release(self.graphs)
+                self.graphs = {}
+        except Exception:  # interpreter shutdown
+            pass
+
     def _val(self, n, ins):
         return ins[n] if n < self.tree.n_in else self.vals[n]
 
@@ -570,6 +602,7 @@ class _TreeRuntime:
         with gc_paused(), torch.cuda.graph(g):
             fn()
         self.graphs[key] = g
+        graphs.drain_deferred()
         g.replay()
 
     def forward(self, ins):

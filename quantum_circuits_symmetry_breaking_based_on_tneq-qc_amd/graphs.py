@@ -19,6 +19,47 @@ from typing import Callable, Sequence, Tuple
 import torch
 
 
+# Releases deferred while a stream capture is in progress: HIP refuses hipGraphExecDestroy /
+# hipFree / hipStreamDestroy during a (global-mode) capture, so an object whose last reference
+# drops inside a caller's `torch.cuda.graph` capture -- a plan, a reverse-tree runtime with its
+# CUDAGraphs -- parks its resources here; they are released at the next call that runs outside a
+# capture (drain_deferred: plan creation / execution, the end of our own capture sites, exit).
+_DEFERRED: list = []
+
+
+def capturing() -> bool:
+    """True while the current stream captures (a caller's torch.cuda.graph block)."""
+    try:
+        return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    except Exception:   # interpreter shutdown
+        return False
+
+
+def defer_release(obj) -> None:
+    """Keep `obj` (a plan handle wrapper or any object holding HIP resources) alive until the
+    next drain outside a capture."""
+    _DEFERRED.append(obj)
+
+
+def drain_deferred() -> int:
+    """Release what was parked during captures (outside a capture only); returns how many
+    objects are still parked."""
+    if not _DEFERRED or capturing():
+        return len(_DEFERRED)
+    items = _DEFERRED[:]
+    del _DEFERRED[:]
+    for it in items:
+        rel = getattr(it, "release_now", None)
+        if rel is not None:
+            rel()                  # may park itself again if HIP still refuses
+    del items                      # the rest (e.g. CUDAGraphs) die here
+    return len(_DEFERRED)
+
+
+def deferred_count() -> int:
+    return len(_DEFERRED)
+
+
 @contextlib.contextmanager
 def gc_paused():
     """Python's cyclic GC off for the duration (wrap a whole ``torch.cuda.graph`` capture in it).
@@ -57,4 +98,5 @@ def capture_step(step_fn: Callable[[], torch.Tensor], params: Sequence[torch.Ten
     with gc_paused(), torch.cuda.graph(g, stream=s):
         loss = step_fn()
     torch.cuda.synchronize(device)
+    drain_deferred()
     return g, loss
