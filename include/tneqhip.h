@@ -146,7 +146,10 @@ int64_t tq_plan_query(tq_plan plan, const char* key);
  * 0 launches them eagerly on the stream (use when the caller captures the stream itself);
  * "sweep_chain" = 1 (default, env TQ_S2_SEQ) runs consecutive hoisted levels that are each one
  * small sweep2 op as one launch of one workgroup (query "n_chain_launches"), 0 one launch per
- * level; "sweep_coop" = 0 (default, env TQ_S2_COOP) -- 1 runs consecutive hoisted levels of
+ * level; "gemm_planes" = 1 (default, env TQ_GEMM_PLANES) runs the plan's boundary GEMM on operands
+ * its dense producers store pre-split as six f16 term planes (query "planes_gemm": planned,
+ * "planes_active", "planes_bytes": the extra device memory), 0 on the GEMM-side split kernel;
+ * "sweep_coop" = 0 (default, env TQ_S2_COOP) -- 1 runs consecutive hoisted levels of
  * multi-chunk sweep2 ops as one launch whose workgroups hand off through a counter barrier
  * (diagnostic: measured slower; a wait that gives up is counted in query "coop_timeouts"). */
 int tq_plan_set(tq_plan plan, const char* key, int64_t value);

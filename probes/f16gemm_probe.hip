@@ -73,8 +73,16 @@ __global__ void __launch_bounds__(NT) gemm(Args g) {
   const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
   const long long k0 = split * g.kchunk;
   const int nk = (int)(g.kchunk / BK);
-  const _Float16* Ab = g.A + ((long long)b * g.K + k0) * g.M + m0;
-  const _Float16* Bb = g.B + ((long long)b * g.K + k0) * g.N + n0;
+  // VAR & 2: the production layout -- per slice lane the six f16 term planes of the operand
+  // interleaved per 32 elements, [k][m / 32][plane][32] (planes re_h, re_l, im_h, im_l, s_h, s_l);
+  // batch entry b = 3 lane + product, and the three term pairs of a product concatenated along K
+  // (plane pairs (h, h), (h, l), (l, h))
+  constexpr bool ILV = (VAR & 2) != 0;
+  const int lane_i = b / 3, prod = b % 3;
+  const _Float16* Ab = ILV ? g.A + (long long)lane_i * (g.K / 3) * g.M * 6
+                           : g.A + ((long long)b * g.K + k0) * g.M + m0;
+  const _Float16* Bb = ILV ? g.B + (long long)lane_i * (g.K / 3) * g.N * 6
+                           : g.B + ((long long)b * g.K + k0) * g.N + n0;
 
   // LDS-DMA: wave-instruction i of wave w fills LDS bytes [(8 i + w) KiB, +1 KiB) = tile rows
   // 2 (8 i + w) and + 1; lane l: row r, 32-B chunk c' = (l & 31) >> 1, half l & 1, which holds
@@ -84,8 +92,14 @@ __global__ void __launch_bounds__(NT) gemm(Args g) {
   for (int i = 0; i < 4; ++i) {
     const int r = 2 * (8 * i + w) + (lane >> 5);
     const int c = ((lane & 31) >> 1) ^ fsw(r);
-    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8);
-    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8);
+    if constexpr (ILV) {
+      const int ma = m0 + c * 16 + (lane & 1) * 8, na_ = n0 + c * 16 + (lane & 1) * 8;
+      goA[i] = (uint32_t)((r * (g.M / 32) + (ma >> 5)) * 192 + (ma & 31));
+      goB[i] = (uint32_t)((r * (g.N / 32) + (na_ >> 5)) * 192 + (na_ & 31));
+    } else {
+      goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8);
+      goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8);
+    }
   }
   // the DMA is issued from inline asm: hipcc would treat an in-flight LDS-DMA as a possible alias
   // of the next ds_read and drain it with vmcnt(0); the waits are placed by hand
@@ -97,8 +111,19 @@ __global__ void __launch_bounds__(NT) gemm(Args g) {
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
   };
   auto stage = [&](int t, int buf) {
-    const _Float16* pa = Ab + (long long)t * BK * g.M;
-    const _Float16* pb = Bb + (long long)t * BK * g.N;
+    const _Float16* pa;
+    const _Float16* pb;
+    if constexpr (ILV) {
+      const long long gk = k0 + (long long)t * BK;           // position along K' = 3 K
+      const long long kk = gk % (g.K / 3);
+      const int term = (int)(gk / (g.K / 3));
+      const int plA = 2 * prod + (term == 2 ? 1 : 0), plB = 2 * prod + (term == 1 ? 1 : 0);
+      pa = Ab + kk * g.M * 6 + plA * 32;
+      pb = Bb + kk * g.N * 6 + plB * 32;
+    } else {
+      pa = Ab + (long long)t * BK * g.M;
+      pb = Bb + (long long)t * BK * g.N;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       glds16(pa + goA[i], buf * 2 * TB + (8 * i + w) * 1024);
@@ -155,6 +180,135 @@ __global__ void __launch_bounds__(NT) gemm(Args g) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
     }
+    // the MFMAs stay above the wait: hipcc would otherwise hoist the wait for the NEXT step's
+    // DMA in front of them and expose its latency every step
+    if constexpr (!(VAR & 8)) __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if constexpr (VAR & 16) {
+    if (tid == 0) {
+      unsigned long long* st = g.stamps + 4 * blockIdx.x;
+      st[0] = t0; st[1] = r0; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + i * 16 + g4 * 4 + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        C[(long long)m * g.N + n] = acc[i][j][r];
+      }
+}
+
+// VAR & 4 (gemm3): the three term products of one real product fused per K-step -- per
+// 32-deep step both term planes (h, l) of A and of B are staged (4 x 16 KiB, two buffers) and a
+// wave runs Ah Bh, Ah Bl, Al Bh (96 MFMAs) from fragments read once.  Operands: per slice lane
+// six planar f16 planes [plane][k][m] (re_h, re_l, im_h, im_l, s_h, s_l); batch entry
+// b = 3 lane + product reads planes 2 product and 2 product + 1.
+constexpr int BK3 = 32, TB3 = BK3 * BM * 2;   // 16 KiB per plane tile
+template <int VAR>
+__global__ void __launch_bounds__(NT) gemm3(Args g) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 4 * TB3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int nt = g.N / BN, ntile = (g.M / BM) * nt;
+  const int tile = L % ntile, grp = L / ntile;
+  const int split = grp % g.splits, b = grp / g.splits;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
+  const long long K1 = g.K / 3;            // k per term plane
+  const long long k0 = split * (K1 / g.splits);
+  const int nk = (int)(K1 / g.splits / BK3);
+  const int lane_i = b / 3, prod = b % 3;
+  const long long psA = K1 * g.M, psB = K1 * g.N;   // plane strides
+  const _Float16* Ah = g.A + (long long)lane_i * 6 * psA + (2 * prod) * psA + k0 * g.M + m0;
+  const _Float16* Bh = g.B + (long long)lane_i * 6 * psB + (2 * prod) * psB + k0 * g.N + n0;
+  uint32_t goA[2], goB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 2 * (8 * i + w) + (lane >> 5);
+    const int c = ((lane & 31) >> 1) ^ fsw(r);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8);
+    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8);
+  }
+  const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
+  auto glds16 = [&](const void* src, unsigned off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  auto stage = [&](int t, int buf) {
+    const _Float16* pa = Ah + (long long)t * BK3 * g.M;
+    const _Float16* pb = Bh + (long long)t * BK3 * g.N;
+    const unsigned o = buf * 4 * TB3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16(pa + goA[i], o + (8 * i + w) * 1024);
+      glds16(pa + psA + goA[i], o + TB3 + (8 * i + w) * 1024);
+      glds16(pb + goB[i], o + 2 * TB3 + (8 * i + w) * 1024);
+      glds16(pb + psB + goB[i], o + 3 * TB3 + (8 * i + w) * 1024);
+    }
+  };
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int x = q | ((g4 & 1) << 2);
+  const int rowb = (8 * g4 + q) * (BM * 2) + 8 * p;
+  int aoff[8], boff[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) aoff[i] = rowb + ((wm * 8 + i) ^ x) * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) boff[j] = 2 * TB3 + rowb + ((wn * 4 + j) ^ x) * 32;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto rd = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BM * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+  };
+  unsigned long long t0 = 0, r0 = 0;
+  if constexpr (VAR & 16) {
+    if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  }
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const char* s = lds + (t & 1) * 4 * TB3;
+    if (t + 1 < nk) stage(t + 1, (t & 1) ^ 1);
+    f16x8 ah[8], al[8], bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bh[j] = rd(s, boff[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ah[i] = rd(s, aoff[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bl[j] = rd(s, boff[j] + TB3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) al[i] = rd(s, aoff[i] + TB3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    // the MFMAs stay above the wait: hipcc would otherwise hoist the wait for the NEXT step's
+    // DMA in front of them and expose its latency every step
+    if constexpr (!(VAR & 8)) __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if constexpr (VAR & 16) {
@@ -177,6 +331,12 @@ __global__ void __launch_bounds__(NT) gemm(Args g) {
 }
 
 template <int VAR>
+static void launch(int nwg, const Args& g) {
+  if constexpr (VAR & 4) hipLaunchKernelGGL(gemm3<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  else hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+}
+
+template <int VAR>
 static void run(const char* name, Args g, int nwg, bool check) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -185,7 +345,7 @@ static void run(const char* name, Args g, int nwg, bool check) {
   CK(hipEventRecord(e0));
   int nw = 0;
   for (;;) {
-    hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+    launch<VAR>(nwg, g);
     ++nw;
     if (nw % 20 == 0) {
       CK(hipEventRecord(e1));
@@ -197,7 +357,7 @@ static void run(const char* name, Args g, int nwg, bool check) {
   }
   const int R = 10;
   CK(hipEventRecord(e0));
-  for (int r = 0; r < R; ++r) hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  for (int r = 0; r < R; ++r) launch<VAR>(nwg, g);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -219,14 +379,32 @@ static void run(const char* name, Args g, int nwg, bool check) {
   double maxrel = -1;
   if (check) {
     // 24 sampled outputs against an f64 host dot product of the same operand values
+    const bool ilv = (VAR & 2) != 0;
     std::vector<float> part((size_t)g.splits);
     maxrel = 0;
     for (int s = 0; s < 24; ++s) {
       const int b = (s * 7) % g.batch, m = (s * 389 + 11) % g.M, n = (s * 613 + 5) % g.N;
       double ref = 0, nrm = 0;
       for (long long k = 0; k < g.K; ++k) {
-        const double a = (double)(_Float16)hval(((uint64_t)b * g.K + k) * g.M + m, 1);
-        const double bb = (double)(_Float16)hval(((uint64_t)b * g.K + k) * g.N + n, 2);
+        uint64_t ia, ib;
+        if (VAR & 4) {
+          const long long K1 = g.K / 3, kk = k % K1;
+          const int term = (int)(k / K1), lane_i = b / 3, prod = b % 3;
+          const int plA = 2 * prod + (term == 2 ? 1 : 0), plB = 2 * prod + (term == 1 ? 1 : 0);
+          ia = (((uint64_t)lane_i * 6 + plA) * K1 + kk) * g.M + m;
+          ib = (((uint64_t)lane_i * 6 + plB) * K1 + kk) * g.N + n;
+        } else if (ilv) {
+          const long long K1 = g.K / 3, kk = k % K1;
+          const int term = (int)(k / K1), lane_i = b / 3, prod = b % 3;
+          const int plA = 2 * prod + (term == 2 ? 1 : 0), plB = 2 * prod + (term == 1 ? 1 : 0);
+          ia = (((uint64_t)lane_i * K1 + kk) * (g.M / 32) + (m >> 5)) * 192 + plA * 32 + (m & 31);
+          ib = (((uint64_t)lane_i * K1 + kk) * (g.N / 32) + (n >> 5)) * 192 + plB * 32 + (n & 31);
+        } else {
+          ia = ((uint64_t)b * g.K + k) * g.M + m;
+          ib = ((uint64_t)b * g.K + k) * g.N + n;
+        }
+        const double a = (double)(_Float16)hval(ia, 1);
+        const double bb = (double)(_Float16)hval(ib, 2);
         ref += a * bb;
         nrm += fabs(a * bb);
       }
@@ -268,5 +446,10 @@ int main(int argc, char** argv) {
   if (v == 0 || v == 1) run<0>("base", g, nwg, true);
   if (v == 0 || v == 2) run<1>("setprio", g, nwg, false);
   if (v == 0 || v == 3) run<16>("base_stamps", g, nwg, false);
+  if (v == 0 || v == 4) run<2>("interleaved_planes", g, nwg, true);
+  if (v == 0 || v == 5) run<18>("interleaved_planes_stamps", g, nwg, false);
+  if (v == 0 || v == 6) run<4>("fused_terms_planar", g, nwg, true);
+  if (v == 0 || v == 7) run<20>("fused_terms_planar_stamps", g, nwg, false);
+  if (v == 0 || v == 8) run<12>("fused_terms_planar_nosb", g, nwg, false);
   return 0;
 }

@@ -242,6 +242,10 @@ int tq_plan_set(tq_plan p, const char* key, int64_t value) {
     p->plan.use_seq = value != 0;
     return TQ_OK;
   }
+  if (k == "gemm_planes") {      // 0: the boundary GEMM on the GEMM-side split kernel
+    p->plan.use_planes = value != 0;
+    return TQ_OK;
+  }
   if (k == "sweep_coop") {       // 0: the multi-chunk sweep2 levels of a chain run one launch each
     p->plan.use_coop = value != 0;
     return TQ_OK;
@@ -300,6 +304,9 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
     return c;
   }
   if (k == "n_launch_slice") return P.n_launch_slice;
+  if (k == "planes_gemm") return P.planes_gemm >= 0 ? 1 : 0;   // a pre-split boundary GEMM was planned
+  if (k == "planes_active") return (P.planes_gemm >= 0 && P.use_planes && (P.d_planes || !P.d_arena)) ? 1 : 0;
+  if (k == "planes_bytes") return (int64_t)P.planes_bytes;
   if (k == "out_numel") return P.out_numel;
   return -1;
 }

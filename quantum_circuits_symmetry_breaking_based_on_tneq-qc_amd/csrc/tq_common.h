@@ -170,6 +170,35 @@ int apply_launch(int dtype, int64_t O, int64_t K1, int64_t M, int64_t K2, int64_
                  const void* S, const void* G, const int32_t* gidx, void* C, double beta,
                  hipStream_t stream);
 int axpy_launch(int dtype, int64_t n, const void* x, void* y, double beta, hipStream_t stream);
+// The boundary GEMM on operands pre-split by their producer into six f16 planes (tq_gemmp.hip):
+// C = A^T B complex64 (K-outer operands), f32 accuracy on the f16 matrix cores (Gauss 3M x 3 term
+// products).  Batch entry b's plane p of A is A + b sA + p psA, element (k, m) at k lda + m
+// (planes re_h, re_l, im_h, im_l, s_h, s_l; s = re + im scaled one binade lower); B likewise.
+struct PlanesGemmArgs {
+  const _Float16* A = nullptr;
+  const _Float16* B = nullptr;
+  int64_t sA = 0, sB = 0, psA = 0, psB = 0, lda = 0, ldb = 0;
+  int M = 0, N = 0, batch = 1, splits = 1;   // splits: set by the launcher
+  int64_t K = 0;
+  float* W = nullptr;                        // partials, planes_gemm_workspace bytes
+};
+// C + j sC (complex64, row stride ldc; one output when lane_sum) = [sum over batch entries j]
+// 2^-(sc_a[j stride] + sc_b[j stride]) x the complex product + beta C
+struct PlanesCombineArgs {
+  const float* W = nullptr;
+  int M = 0, N = 0, batch = 1, splits = 1;   // set by the launcher
+  const int32_t* sc_a = nullptr;
+  const int32_t* sc_b = nullptr;
+  int64_t sc_stride = 0;
+  void* C = nullptr;
+  int64_t ldc = 0, sC = 0;
+  int lane_sum = 0;
+  float beta = 0.f;
+};
+bool planes_gemm_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+int planes_gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch);
+size_t planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch);
+int planes_gemm_launch(const PlanesGemmArgs& a, const PlanesCombineArgs& c, hipStream_t stream);
 // y[i] = sum_{j < nl} y[i + j * stride] (elements), i < n: slice lanes summed into lane 0
 int lane_sum_launch(int dtype, int64_t n, void* y, int64_t stride, int nl, hipStream_t stream);
 // measurement data (tq_data.hip)

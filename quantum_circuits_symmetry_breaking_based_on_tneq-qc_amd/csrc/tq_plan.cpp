@@ -414,10 +414,76 @@ class Compiler {
         if (std::find(v.begin(), v.end(), j) == v.end()) v.push_back(j);
       }
     }
+    // the pre-split boundary GEMM (tq_gemmp.hip): a per-slice GEMM whose operands are each stored
+    // in full by one per-slice dense sweep op and read by nothing else; those ops then store the
+    // operand as six f16 term planes, scaled from a bound built on the max of their own input,
+    // whose producer (a sweep2 op storing exactly that input) gets a max word too.  The largest
+    // such GEMM of the plan (C4 / C3: the boundary contraction of the cut network)
+    P_.planes_gemm = -1;
+    std::vector<int> planes_x(P_.ops.size(), -1);
+    if (planes_enabled()) {
+      auto only_reader = [&](int j, int gi) {
+        int sp, spo;
+        int64_t lo, hi, olo, ohi;
+        const Op& w = P_.ops[j];
+        if (!span(w.c, w.nc, &sp, &lo, &hi)) return false;
+        auto hits = [&](const BufRef& r, int64_t n) {
+          return span(r, n, &spo, &olo, &ohi) && spo == sp && olo < hi && lo < ohi;
+        };
+        for (size_t k = j + 1; k < P_.ops.size(); ++k) {
+          const Op& o = P_.ops[k];
+          if ((int)k != gi) {
+            if (hits(o.a, o.na) || hits(o.b, o.nb) || (o.kind == OP_AXPY && hits(o.c, o.nc))) return false;
+            for (auto& g : o.sgates) if (hits(g.g, std::max<int64_t>(g.n, 1))) return false;
+          }
+          if (hits(o.c, o.nc) || (o.nws && hits(o.ws, o.nws))) break;
+        }
+        return true;
+      };
+      double best = 0;
+      for (size_t i = 0; i < P_.ops.size(); ++i) {
+        const Op& g = P_.ops[i];
+        const int pa = prod_a[i], pb = prod_b[i];
+        if (pa < 0 || pa == pb || g.invariant || g.batch != 1 || g.writes_output || g.skinny) continue;
+        if (!planes_gemm_ok(g.M, g.N, g.K, g.lda, g.ldb)) continue;
+        const Op& da = P_.ops[pa];
+        const Op& db = P_.ops[pb];
+        if (!da.s2_dense || !db.s2_dense || da.invariant || db.invariant || da.writes_output || db.writes_output) continue;
+        if (!only_reader(pa, (int)i) || !only_reader(pb, (int)i)) continue;
+        const int xa = producer(pa, da.a, da.na), xb = producer(pb, db.a, db.na);
+        if (xa < 0 || xb < 0 || P_.ops[xa].s2_dense || P_.ops[xb].s2_dense) continue;
+        if (P_.ops[xa].invariant != P_.ops[xb].invariant) continue;
+        const double w = (double)g.M * g.N * g.K;
+        if (w > best) {
+          best = w;
+          P_.planes_gemm = (int)i;
+          planes_x[pa] = xa;
+          planes_x[pb] = xb;
+        }
+      }
+      if (P_.planes_gemm >= 0) {
+        const Op& g = P_.ops[P_.planes_gemm];
+        const int pab[2] = {prod_a[P_.planes_gemm], prod_b[P_.planes_gemm]};
+        for (int r = 0; r < 2; ++r) {
+          const int j = pab[r], x = planes_x[j];
+          P_.ops[j].planes_role = r + 1;
+          auto& v = P_.ops[x].invariant ? once : slice;
+          if (std::find(v.begin(), v.end(), x) == v.end()) v.push_back(x);
+          // the planes (12 B per element) replace the complex64 store (8 B)
+          P_.ops[j].bytes += (double)P_.ops[j].nc * 4.0;
+          P_.ops[j].note += r ? " planes(B)" : " planes(A)";
+        }
+        P_.planes_n[0] = g.na;
+        P_.planes_n[1] = g.nb;
+        P_.ops[P_.planes_gemm].note += " planes";
+      }
+    }
     P_.n_amax_once = (int)once.size();
     P_.n_amax_slice = (int)slice.size();
     for (size_t q = 0; q < once.size(); ++q) P_.ops[once[q]].amax_word = (int)q;
     for (size_t q = 0; q < slice.size(); ++q) P_.ops[slice[q]].amax_word = P_.n_amax_once + (int)q;
+    for (size_t j = 0; j < P_.ops.size(); ++j)
+      if (P_.ops[j].planes_role) P_.ops[j].planes_in_amax = P_.ops[planes_x[j]].amax_word;
     for (size_t i = 0; i < P_.ops.size(); ++i) {
       if (prod_a[i] < 0) continue;
       P_.ops[i].amax_a = P_.ops[prod_a[i]].amax_word;
@@ -450,6 +516,7 @@ class Compiler {
       Op& g = P_.ops[i];
       const int pa = prod_a[i], pb = prod_b[i];
       if (pa < 0 || pa == pb || g.invariant || g.batch != 1 || P_.n_slices > max_slices) continue;
+      if ((int)i == P_.planes_gemm) continue;
       if (P_.ops[pa].invariant || P_.ops[pb].invariant) continue;
       if (P_.ops[pa].ps_gemm >= 0 || P_.ops[pb].ps_gemm >= 0) continue;
       if (!exclusive(pa, (int)i) || !exclusive(pb, (int)i)) continue;
@@ -1217,6 +1284,14 @@ class Compiler {
   static bool s2_enabled() {
     static const int v = [] {
       const char* e = getenv("TQ_SWEEP2");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v != 0;
+  }
+  // the pre-split boundary GEMM (TQ_GEMM_PLANES=0: the GEMM-side split kernel instead)
+  static bool planes_enabled() {
+    static const int v = [] {
+      const char* e = getenv("TQ_GEMM_PLANES");
       return (e && e[0] == '0') ? 0 : 1;
     }();
     return v != 0;
@@ -2331,6 +2406,20 @@ int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
     TQ_HIP(hipStreamSynchronize(stream));
   }
   if (P.n_ps && !P.h_bad) TQ_HIP(hipHostMalloc((void**)&P.h_bad, P.n_slices * sizeof(uint32_t), hipHostMallocDefault));
+  // the pre-split boundary GEMM's planes, partials and scale words (plan-owned plans only)
+  if (P.planes_gemm >= 0 && P.owns_device && !P.d_planes) {
+    const Op& g = P.ops[P.planes_gemm];
+    const size_t lanes = (size_t)std::max(1, P.lanes);
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    P.planes_lane_bytes = al((size_t)12 * (size_t)(P.planes_n[0] + P.planes_n[1]));
+    P.planes_ws_off = lanes * P.planes_lane_bytes;
+    P.planes_sc_off = P.planes_ws_off + al(planes_gemm_workspace(g.M, g.N, g.K, (int64_t)lanes));
+    P.planes_bytes = P.planes_sc_off + al(lanes * 2 * sizeof(int32_t));
+    if (hipMalloc(&P.d_planes, P.planes_bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      P.d_planes = nullptr;   // no room: the GEMM-side split path runs instead
+    }
+  }
   return TQ_OK;
 }
 
@@ -2427,12 +2516,18 @@ int plan_release(Plan& P) {
     P.d_arena = P.d_tables = nullptr;
   }
   if (P.h_bad && rel(hipHostFree(P.h_bad), "host flag", rc)) P.h_bad = nullptr;
+  if (P.d_planes && rel(hipFree(P.d_planes), "planes", rc)) P.d_planes = nullptr;
   return rc;
 }
 
 
 int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
                  int64_t s_step, int accumulate, hipStream_t stream);
+// the pre-split boundary GEMM runs: the plan has one, its buffers exist, the plan option is on
+// and the pre-split (predicted-scale) mode of the split kernel is not running
+static bool planes_active(const Plan& P) {
+  return P.planes_gemm >= 0 && P.d_planes != nullptr && P.use_planes && !P.run_mode;
+}
 int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
                 int64_t s_step, int accumulate, hipStream_t stream);
 
@@ -2495,6 +2590,7 @@ int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, 
   key.inputs.assign(inputs, inputs + P.n_inputs);
   key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
   key.mode = P.run_mode;
+  key.planes = planes_active(P) ? 1 : 0;
   key.seq = P.use_seq;
   key.coop = P.use_coop;
   constexpr size_t kMaxGraphs = 8;
@@ -2593,8 +2689,45 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
     auto sc_word = [&](int w) { return reinterpret_cast<int32_t*>((char*)P.d_tables + P.sc_off) + (w - P.n_amax_once); };
     auto bad_word = [&](int64_t q) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.bad_off) + q; };
     int lane_gemm = 1;   // > 1: the GEMM launch below covers that many lanes
+    // the pre-split boundary GEMM: lane j's planes of operand r (0 = A, 1 = B) and scale words
+    const bool planes_on = planes_active(P);
+    auto planes_ptr = [&](int j, int r) {
+      return reinterpret_cast<_Float16*>((char*)P.d_planes + (size_t)j * P.planes_lane_bytes +
+                                         (r ? (size_t)12 * P.planes_n[0] : 0));
+    };
+    auto planes_sc = [&](int j, int r) {
+      return reinterpret_cast<int32_t*>((char*)P.d_planes + P.planes_sc_off) + 2 * j + r;
+    };
     auto launch_one = [&](const Op& op, hipStream_t st) -> int {
       const double beta = op.writes_output ? beta_out : 0.0;
+      if (planes_on && op.kind == OP_GEMM && &op == &P.ops[P.planes_gemm]) {
+        // lane batch: entries = the batch's lanes (planes and scale words at their lane strides),
+        // the combine sums them into lane 0's result when the plan sums the lanes (Op::lane_sum)
+        const int j0 = lane_gemm > 1 ? 0 : cur;
+        PlanesGemmArgs a;
+        a.A = planes_ptr(j0, 0);
+        a.B = planes_ptr(j0, 1);
+        a.sA = a.sB = (int64_t)(P.planes_lane_bytes / 2);
+        a.psA = P.planes_n[0];
+        a.psB = P.planes_n[1];
+        a.lda = op.lda;
+        a.ldb = op.ldb;
+        a.M = (int)op.M;
+        a.N = (int)op.N;
+        a.K = op.K;
+        a.batch = lane_gemm;
+        a.W = reinterpret_cast<float*>((char*)P.d_planes + P.planes_ws_off);
+        PlanesCombineArgs c;
+        c.sc_a = planes_sc(j0, 0);
+        c.sc_b = planes_sc(j0, 1);
+        c.sc_stride = 2;
+        c.C = ptr(op.c);
+        c.ldc = op.ldc;
+        c.sC = (int64_t)(P.lane_stride / esz);
+        c.lane_sum = lane_gemm > 1 && op.lane_sum;
+        c.beta = (float)beta;
+        return planes_gemm_launch(a, c, st);
+      }
       switch (op.kind) {
         case OP_PERMUTE:
           TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm],
@@ -2858,6 +2991,13 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
             o.use_beta = o.beta != 0.0;
             o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
             o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
+            if (planes_on && op.planes_role) {
+              o.planes = planes_ptr(cur, op.planes_role - 1);
+              o.pstride = P.planes_n[op.planes_role - 1];
+              o.amax_in = amax_lane(op.planes_in_amax, cur);
+              o.sc_out = planes_sc(cur, op.planes_role - 1);
+              o.amax = nullptr;
+            }
           }
           TQ_TRY(sweepd_launch(P.dtype, L, stream));
           dense.swap(rest);
@@ -2929,8 +3069,10 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
         lane_gemm = 1;
         TQ_TRY(rc);
         if (op0.lane_sum) {
-          TQ_TRY(lane_sum_launch(P.dtype, op0.nc, ptr(op0.c), (int64_t)(P.lane_stride / esz),
-                                 (int)lane_sl.size(), stream));
+          // (the pre-split GEMM's combine has summed the lanes already)
+          if (!(planes_on && grp[0] == P.planes_gemm))
+            TQ_TRY(lane_sum_launch(P.dtype, op0.nc, ptr(op0.c), (int64_t)(P.lane_stride / esz),
+                                   (int)lane_sl.size(), stream));
           lanes_summed = true;
         }
       } else if (op0.lane_once && lanes_summed) {

@@ -82,6 +82,12 @@ struct Op {
   // (ps_cand); its producers (ps_gemm = that GEMM) then store the terms (S2Op::split_sc)
   bool ps_cand = false;
   int ps_gemm = -1;
+  // pre-split boundary GEMM ("planes", tq_gemmp.hip): the GEMM (Plan::planes_gemm) and its two
+  // dense producers (planes_role 1 = A, 2 = B), which then store the six f16 term planes of their
+  // output instead of the complex64 values; planes_in_amax = the max word of the dense op's input
+  // (written by that input's producer) from which the producer bounds its output
+  int planes_role = 0;
+  int planes_in_amax = -1;
   // per-slice GEMM on lane-local (or pinned) operands: the lanes of a batch run as ONE batched
   // launch (strides = Plan::lane_stride, workspace at Plan::lane_ws_off)
   bool lane_batch = false;
@@ -137,6 +143,14 @@ struct Plan {
   int n_ps = 0;               // pre-split candidate GEMMs
   uint32_t* h_bad = nullptr;  // pinned, n_slices words
   int run_mode = 0;           // 1: this execute call runs the candidates pre-split
+  // pre-split boundary GEMM (Op::planes_role): one per plan; device buffer d_planes (plan-owned,
+  // allocated at materialize) = per lane [A planes][B planes] (6 planes of the operand's element
+  // count each, 2 B), then the GEMM's f32 partials, then per lane two scale words (A, B)
+  int planes_gemm = -1;
+  int64_t planes_n[2] = {0, 0};     // elements of the A / B operand (one plane)
+  size_t planes_lane_bytes = 0, planes_ws_off = 0, planes_sc_off = 0, planes_bytes = 0;
+  void* d_planes = nullptr;
+  bool use_planes = true;           // TQ_GEMM_PLANES (default 1) / tq_plan_set "gemm_planes"
   int64_t ps_fallbacks = 0;   // slices re-run on the split path (operand max left the window)
   size_t arena_bytes = 0;
   size_t pinned_base = 0;             // pinned (hoisted, slice-invariant) results live above this
@@ -191,11 +205,12 @@ struct Plan {
     int64_t b = 0, e = 0, s = 0;
     int acc = 0;
     int mode = 0;   // Plan::run_mode the graph was captured with
+    int planes = 0; // the pre-split boundary GEMM was on
     bool seq = true;  // Plan::use_seq
     bool coop = false;  // Plan::use_coop
     bool operator==(const GraphKey& o) const {
       return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc &&
-             mode == o.mode && seq == o.seq && coop == o.coop;
+             mode == o.mode && seq == o.seq && coop == o.coop && planes == o.planes;
     }
   };
   bool use_graph = true;

@@ -201,6 +201,14 @@ struct S2DOp {
   uint32_t* amax = nullptr;        // as S2Op::amax
   const int32_t* split_sc = nullptr;  // as S2Op::split_sc
   int order = 0, pad2 = 0;         // tile order (tq_sweepd.hip): 0 grid-strided, 1 blocked
+  // planes mode (the pre-split boundary GEMM, tq_gemmp.hip): Y is not written; instead the six f16
+  // term planes (re_h, re_l, im_h, im_l, s_h, s_l) of Y * 2^sc go to planes + p * pstride (element
+  // offsets as Y's), sc from the bound max|Y| <= sqrt(2) max(|re X|, |im X|) max_r sum_k |M[r][k]|
+  // (amax_in: X's producer's max word); sc is stored to *sc_out for the GEMM's unscaling
+  void* planes = nullptr;
+  int64_t pstride = 0;
+  const uint32_t* amax_in = nullptr;
+  int32_t* sc_out = nullptr;
 };
 struct S2DLaunch {
   int nops = 0, pad = 0;

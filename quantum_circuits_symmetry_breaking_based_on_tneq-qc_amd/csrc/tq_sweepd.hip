@@ -73,6 +73,10 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 template <int TMAX>
 struct SdSmem {
   float mp[2][TMAX * kS2DMaxTout];
+  float red[kWaves];
+  // planes mode: a wave's [32 rows][8 x 16-B pieces] image of one plane (pieces XOR-swizzled by
+  // row), so that every store instruction writes 8 whole 128-byte row segments
+  uint4 stage[kWaves][32 * 8];
   int32_t ooff[kS2DMaxTout];
   int64_t btab[2][kLevels][64];
   int64_t wcol[2][kS2MaxColBits];
@@ -103,6 +107,35 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
       wcol[i / kS2MaxColBits][i % kS2MaxColBits] = (i / kS2MaxColBits) ? d->w_out[i % kS2MaxColBits] : d->w_in[i % kS2MaxColBits];
   }
   __syncthreads();
+  // planes mode: the operand scale from an a-priori bound of the output, identical in every
+  // workgroup of the op (so every lane of the operand is scaled alike)
+  const bool planes = op.planes != nullptr;
+  int psc = 0;
+  if (planes) {
+    float rs = 0.f;
+    for (int r = tid; r < tout; r += 64 * kWaves) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < TIN; ++k) a += sqrtf(mp[0][k * tout + r] * mp[0][k * tout + r] + mp[1][k * tout + r] * mp[1][k * tout + r]);
+      rs = fmaxf(rs, a);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) rs = fmaxf(rs, __shfl_xor(rs, o));
+    if ((tid & 63) == 0) sm.red[tid >> 6] = rs;
+    __syncthreads();
+    rs = sm.red[0];
+#pragma unroll
+    for (int i = 1; i < kWaves; ++i) rs = fmaxf(rs, sm.red[i]);
+    // |Y| <= |X|max * rs, |X|max <= sqrt(2) max(|re|, |im|); margin for the rounding of the bound
+    const float bound = __uint_as_float(*op.amax_in) * 1.41421356f * rs * 1.001f;
+    const uint32_t bits = __float_as_uint(bound);
+    const int E = (int)((bits >> 23) & 0xff);
+    if (bits != 0 && E != 255) {
+      const int e = E ? E - 127 : (31 - __clz((int)(bits & 0x7fffff))) - 149;
+      psc = 14 - e;   // bound * 2^psc in [2^14, 2^15): no f16 overflow (65504)
+    }
+    if (blockIdx.x == (unsigned)op.block_begin && tid == 0) *op.sc_out = psc;
+  }
   // btab[io][l][v] = sum of the weights of the set bits of v among column bits 6+6l .. 6+6l+5
   for (int i = tid; i < 2 * kLevels * 64; i += 64 * kWaves) {
     const int io = i / (kLevels * 64), l = (i / 64) % kLevels, v = i % 64;
@@ -164,6 +197,66 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
       else if (w.x == 12345.f) *p = w;
     }
   };
+  // planes mode: per wave a 64-column group (both 32-column tiles of a column-bit-5 pair) and 32
+  // output rows at a time, computed transposed (D^T[c][r]: lane = row rt + (lane & 31), registers =
+  // columns (e & 3) + 8 (e >> 2) + 4 fk); a permlane32 swap per register pair leaves every lane two
+  // runs of 8 consecutive columns per tile; per plane the four 16-B runs of a lane go to the wave's
+  // LDS image and come back so that 8 lanes hold one row's 128 B: each store instruction writes
+  // 8 whole 128-byte lines of the plane (the rows' 64-element runs are contiguous and aligned)
+  auto emit_planes = [&](f32x16 (&d)[2][2], int64_t gbase, int rt) {
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int a = 8 * h + i, b = 8 * h + 4 + i;
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(d[tl][ri][a]), __float_as_uint(d[tl][ri][b]), false, false);
+            d[tl][ri][a] = __uint_as_float(sw[0]);
+            d[tl][ri][b] = __uint_as_float(sw[1]);
+          }
+    uint4* st = sm.stage[wave];
+    _Float16* P = reinterpret_cast<_Float16*>(op.planes);
+    const int row_w = fr;                       // this lane's row in the image (write side)
+    const int row_r = lane >> 3, pc_r = lane & 7;   // read side: 8 lanes per row
+    int64_t so[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) so[q] = gbase + ooff[rt + 8 * q + row_r] + 8 * pc_r;
+#pragma unroll
+    for (int pl = 0; pl < 6; ++pl) {
+      // the lane's 4 pieces of this plane: tile tl, run h -> piece 4 tl + 2 h + fk (columns 8 x piece)
+#pragma unroll
+      for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t w4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int e0 = 8 * h + 2 * j;
+            const f2v re = {d[tl][0][e0], d[tl][0][e0 + 1]}, im = {d[tl][1][e0], d[tl][1][e0 + 1]};
+            f2v t;
+            if (pl < 2) t = f16_terms(re, psc);
+            else if (pl < 4) t = f16_terms(im, psc);
+            else t = f16_terms(re + im, psc - 1);
+            w4[j] = __float_as_uint((pl & 1) ? t.y : t.x);
+          }
+          const int pc = 4 * tl + 2 * h + fk;
+          st[row_w * 8 + (pc ^ (row_w & 7))] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's image is complete (wave-private)
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 8 * q + row_r;
+        const uint4 v = st[r * 8 + (pc_r ^ (r & 7))];
+        *reinterpret_cast<uint4*>(P + pl * op.pstride + so[q]) = v;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // reads done before the next plane's writes
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
   // tile order: grid-strided (default: concurrently running workgroups write neighbouring 1-KiB
   // pieces of the same output rows) or blocked (op.order == 1, TQ_S2D_BLOCKED=1: each workgroup
   // walks its own contiguous range of tiles, i.e. whole runs of one row set)
@@ -174,6 +267,43 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
     t0 = blk * per + wave;
     t_end = ntiles < (blk + 1) * per ? ntiles : (blk + 1) * per;
     t_step = kWaves;
+  }
+  if (planes) {
+    // 64-column groups (column bits 0..5), the same products with the operands swapped (the
+    // transposed tile: columns in registers)
+    const int64_t ngroups = ntiles >> 1;
+    for (int64_t g = (int64_t)blk * kWaves + wave; g < ngroups; g += nw) {
+      const int64_t bi = base(0, g);
+      float xr[2][KS], xi[2][KS];
+#pragma unroll
+      for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const f2v v = X[bi + io[s] + 32 * tl + fr];
+          xr[tl][s] = v.x;
+          xi[tl][s] = v.y;
+        }
+      const int64_t gb = base(1, g);
+      for (int rt = 0; rt < tout; rt += 32) {
+        f32x16 d[2][2];
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl) {
+          f32x16 p1 = {}, p2 = {}, p3 = {};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const int a = (2 * s + fk) * tout + rt + fr;
+            const float mr = mp[0][a], mi = mp[1][a];
+            p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[tl][s], mr, p1, 0, 0, 0);
+            p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(xi[tl][s], mi, p2, 0, 0, 0);
+            p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[tl][s] + xi[tl][s], mr + mi, p3, 0, 0, 0);
+          }
+          d[tl][0] = p1 - p2;
+          d[tl][1] = p3 - p1 - p2;
+        }
+        emit_planes(d, gb, rt);
+      }
+    }
+    return;
   }
   for (int64_t t = t0; t < t_end; t += t_step) {
     // column tile t: columns 32t .. 32t+31 (bits 0..4 = lane, bit 5 = t & 1, bits >= 6: tables)

@@ -170,6 +170,9 @@ def _production_plan_checks(e, cfg, lanes):
         # mixed sweepd launch, tq_sweepd.hip)
         dense = [l for l in d.splitlines() if "SWEEP2 DENSE" in l]
         assert any("tin=16" in l for l in dense) and any("tin=8" in l for l in dense), dense
+        # the boundary GEMM on operands pre-split by those dense ops (tq_gemmp.hip)
+        assert plan.query("planes_gemm") == 1, d
+        assert any("planes(A)" in l for l in dense) and any("planes(B)" in l for l in dense), dense
 
 
 @pytest.mark.timeout(900)
@@ -195,6 +198,33 @@ def test_bench_launch_vs_oracle(dev, cfg, lanes):
     for r in res:
         _check(r, ref, TOL["complex64"], cfg)
     assert np.array_equal(res[1], res[2])   # replays are deterministic
+
+
+@pytest.mark.timeout(900)
+def test_planes_gemm_equals_split_kernel(dev):
+    """C4's boundary GEMM on producer-split operands (the dense ops store six f16 term planes
+    scaled from a bound of their output; tq_gemmp.hip: Gauss 3M x 3 term products from LDS-DMA
+    staged planes, split-K partials, one combine pass summing the lanes) against the same plan on
+    the GEMM-side split kernel ("gemm_planes" = 0) and both against the oracle's sum over all
+    slices.  The two kernels round differently (the planes' scale comes from a bound, not the
+    true max), so they agree to the complex64 tolerance, not bitwise."""
+    import torch
+    from tneq_qc_amd.circuits import config_task
+    t = config_task("C4")
+    e, ops = _expr_and_ops(t, dev, torch.complex64)
+    plan = e.plan(torch.complex64)
+    assert plan.query("planes_gemm") == 1
+    on = e(*ops).cpu().numpy()
+    assert plan.query("planes_active") == 1 and plan.query("planes_bytes") > 0
+    plan.set("gemm_planes", 0)
+    off = e(*ops).cpu().numpy()
+    plan.set("gemm_planes", 1)
+    again = e(*ops).cpu().numpy()
+    ref = _oracle_full("C4")
+    _check(on, ref, TOL["complex64"], "planes")
+    _check(off, ref, TOL["complex64"], "split")
+    assert np.abs(on - off).max() / np.abs(ref).max() < TOL["complex64"]
+    assert np.array_equal(on, again)
 
 
 @pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 4)])
