@@ -416,17 +416,28 @@ def main():
     bf16 = bool(L.tq_library_query(b"gemm_bf16") == 1)
     f16 = bf16 and bool(L.tq_library_query(b"gemm_f16") == 1)
     f16_g3 = f16 and L.tq_library_query(b"gemm_f16_var") in (2, 5, 6, 7, 8, 9)   # Gauss 3M on the f16 terms
+    planes = plan.query("planes_active") == 1   # the pre-split boundary GEMM (tq_gemmp.hip)
     value = n_amp * args.steps / dt
     nl = max(1, gemm["launches"])
     avg_gemm_s = gemm["ms"] / 1e3 / nl
     alg_flops = gemm["flops"] / nl                      # 8*M*N*K complex GEMM flops per launch
     # MFMA work executed per launch: f16 split = 4 real products x 3 term products = 24*M*N*K;
     # bf16 split = 4 x 6 = 48*M*N*K; f32 3M = 6*M*N*K, f32 4M = 8*M*N*K
-    exe_flops = alg_flops * (2.25 if f16_g3 else 3.0 if f16 else 6.0 if bf16 else (0.75 if g3m else 1.0))
+    exe_flops = alg_flops * (2.25 if (planes or f16_g3) else 3.0 if f16 else 6.0 if bf16 else (0.75 if g3m else 1.0))
     peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     achieved = exe_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
     alg_rate = alg_flops / avg_gemm_s / 1e12 if avg_gemm_s > 0 else 0.0
-    if f16:
+    if planes:
+        peak = PEAK_BF16_MFMA_TFLOPS
+        pmc_b = _profile_json("pmc_gemm_planes_r05.json", args.config)
+        pmc_t = pmc_b
+        kdesc = ("boundary GEMM on pre-split operands (complex64: the dense producers store each operand as six "
+                 "f16 term planes of its power-of-two-scaled re, im, re+im; Gauss's 3 real products x 3 term "
+                 "products (hh, hl, lh) on v_mfma_f32_16x16x32_f16, f32 accumulation, LDS-DMA staged 256x256 "
+                 "tiles, split-K partials + one combine pass that also sums the slice lanes)")
+        exe_def = ("executed f16 MFMA flops per launch (3 real products (Gauss) x 3 term products = 18*M*N*K) / "
+                   "avg launch time of the GEMM + combine")
+    elif f16:
         pmc_b = _profile_json("pmc_gemm_f16_r04g.json" if f16_g3 else "pmc_gemm_f16_r02.json", args.config)
         pmc_t = pmc_b
         kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_f16: every f32 operand scaled by a power of two "

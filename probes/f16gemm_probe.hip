@@ -233,15 +233,16 @@ __global__ void __launch_bounds__(NT) gemm3(Args g) {
   for (int i = 0; i < 2; ++i) {
     const int r = 2 * (8 * i + w) + (lane >> 5);
     const int c = ((lane & 31) >> 1) ^ fsw(r);
-    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8);
-    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8) * 2;   // bytes
+    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8) * 2;
   }
   const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
-  auto glds16 = [&](const void* src, unsigned off) {
+  // SGPR base + 32-bit lane byte offset (global_load_lds_dwordx4 v, s[]): no 64-bit address VGPRs
+  auto glds16 = [&](const _Float16* base, uint32_t voff, unsigned off) {
     unsigned keep;
     const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(base), "s"(dst) : "memory");
   };
   auto stage = [&](int t, int buf) {
     const _Float16* pa = Ah + (long long)t * BK3 * g.M;
@@ -249,10 +250,10 @@ __global__ void __launch_bounds__(NT) gemm3(Args g) {
     const unsigned o = buf * 4 * TB3;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      glds16(pa + goA[i], o + (8 * i + w) * 1024);
-      glds16(pa + psA + goA[i], o + TB3 + (8 * i + w) * 1024);
-      glds16(pb + goB[i], o + 2 * TB3 + (8 * i + w) * 1024);
-      glds16(pb + psB + goB[i], o + 3 * TB3 + (8 * i + w) * 1024);
+      glds16(pa, goA[i], o + (8 * i + w) * 1024);
+      glds16(pa + psA, goA[i], o + TB3 + (8 * i + w) * 1024);
+      glds16(pb, goB[i], o + 2 * TB3 + (8 * i + w) * 1024);
+      glds16(pb + psB, goB[i], o + 3 * TB3 + (8 * i + w) * 1024);
     }
   };
   const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -330,9 +331,159 @@ __global__ void __launch_bounds__(NT) gemm3(Args g) {
       }
 }
 
+// VAR & 32 (gemm4): gemm3 with the barrier between the 2nd and 3rd term products and the next
+// step's ah / bh fragments read under the 3rd term's MFMAs (into the registers the 2nd term
+// freed): a step starts multiplying at once; two register roles alternate (unroll 2)
+template <int VAR>
+__global__ void __launch_bounds__(NT) gemm4(Args g) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 4 * TB3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int nt = g.N / BN, ntile = (g.M / BM) * nt;
+  const int tile = L % ntile, grp = L / ntile;
+  const int split = grp % g.splits, b = grp / g.splits;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
+  const long long K1 = g.K / 3;
+  const long long k0 = split * (K1 / g.splits);
+  const int nk = (int)(K1 / g.splits / BK3);
+  const int lane_i = b / 3, prod = b % 3;
+  const long long psA = K1 * g.M, psB = K1 * g.N;
+  const _Float16* Ah = g.A + (long long)lane_i * 6 * psA + (2 * prod) * psA + k0 * g.M + m0;
+  const _Float16* Bh = g.B + (long long)lane_i * 6 * psB + (2 * prod) * psB + k0 * g.N + n0;
+  uint32_t goA[2], goB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 2 * (8 * i + w) + (lane >> 5);
+    const int c = ((lane & 31) >> 1) ^ fsw(r);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8) * 2;   // bytes
+    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8) * 2;
+  }
+  const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
+  // SGPR base + 32-bit lane byte offset (global_load_lds_dwordx4 v, s[]): no 64-bit address VGPRs
+  auto glds16 = [&](const _Float16* base, uint32_t voff, unsigned off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(base), "s"(dst) : "memory");
+  };
+  auto stage = [&](int t, int buf) {
+    const _Float16* pa = Ah + (long long)t * BK3 * g.M;
+    const _Float16* pb = Bh + (long long)t * BK3 * g.N;
+    const unsigned o = buf * 4 * TB3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16(pa, goA[i], o + (8 * i + w) * 1024);
+      glds16(pa + psA, goA[i], o + TB3 + (8 * i + w) * 1024);
+      glds16(pb, goB[i], o + 2 * TB3 + (8 * i + w) * 1024);
+      glds16(pb + psB, goB[i], o + 3 * TB3 + (8 * i + w) * 1024);
+    }
+  };
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int x = q | ((g4 & 1) << 2);
+  const int rowb = (8 * g4 + q) * (BM * 2) + 8 * p;
+  // chunk (wm 8 + i) ^ x = wm 8 + (i ^ x): offset = abase ^ (i << 5) (bits 5..7 of rowb are 0);
+  // B: chunk (wn 4 + j) ^ x -> bbase ^ (j << 5).  Re-derived per read (one v_xor) instead of 12
+  // loop-invariant address registers
+  const int abase = (rowb + ((wm * 8) ^ x) * 32);
+  const int bbase = 2 * TB3 + rowb + ((wn * 4) ^ x) * 32;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto rd = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BM * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+  };
+  int aoffv[8], boffv[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) aoffv[i] = abase ^ (i << 5);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) boffv[j] = bbase ^ (j << 5);
+  auto aoff = [&](int i) { return aoffv[i]; };
+  auto boff = [&](int j) { return boffv[j]; };
+  auto mm = [&](const f16x8 (&a)[8], const f16x8 (&bb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], bb[j], acc[i][j], 0, 0, 0);
+  };
+  // registers: A (8 fragments: this step's ah, replaced row by row by al during the hl
+  // products, then by the next step's ah during the lh products), two B sets whose roles (bh / bl)
+  // alternate every step: the next bh is read during the lh products into the set bl held
+  f16x8 A[8], B0[4], B1[4];
+  unsigned long long t0 = 0, r0 = 0;
+  if constexpr (VAR & 16) {
+    if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  }
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) B0[j] = rd(lds, boff(j));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) A[i] = rd(lds, aoff(i));
+  auto step = [&](int t, f16x8 (&BH)[4], f16x8 (&BL)[4]) {
+    const char* s = lds + (t & 1) * 4 * TB3;
+    const char* sn = lds + ((t & 1) ^ 1) * 4 * TB3;
+    if (t + 1 < nk) stage(t + 1, (t & 1) ^ 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) BL[j] = rd(s, boff(j) + TB3);
+    mm(A, BH);                                   // h h
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                // h l, row i's ah replaced by its al
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[i], BL[j], acc[i][j], 0, 0, 0);
+      A[i] = rd(s, aoff(i) + TB3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the next buffer landed for every wave; this buffer's reads are done
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // (past the last step these read the idle buffer: harmless, unused)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) BL[j] = rd(sn, boff(j));     // the next step's bh
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                // l h, row i's al replaced by the next ah
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[i], BH[j], acc[i][j], 0, 0, 0);
+      A[i] = rd(sn, aoff(i));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (int t = 0; t < nk; t += 2) {   // nk even (launcher)
+    step(t, B0, B1);
+    step(t + 1, B1, B0);
+  }
+  if constexpr (VAR & 16) {
+    if (tid == 0) {
+      unsigned long long* st = g.stamps + 4 * blockIdx.x;
+      st[0] = t0; st[1] = r0; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + i * 16 + g4 * 4 + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        C[(long long)m * g.N + n] = acc[i][j][r];
+      }
+}
+
 template <int VAR>
 static void launch(int nwg, const Args& g) {
-  if constexpr (VAR & 4) hipLaunchKernelGGL(gemm3<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  if constexpr (VAR & 32) hipLaunchKernelGGL(gemm4<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  else if constexpr (VAR & 4) hipLaunchKernelGGL(gemm3<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
   else hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
 }
 
@@ -451,5 +602,7 @@ int main(int argc, char** argv) {
   if (v == 0 || v == 6) run<4>("fused_terms_planar", g, nwg, true);
   if (v == 0 || v == 7) run<20>("fused_terms_planar_stamps", g, nwg, false);
   if (v == 0 || v == 8) run<12>("fused_terms_planar_nosb", g, nwg, false);
+  if (v == 0 || v == 9) run<36>("pipelined_terms", g, nwg, true);
+  if (v == 0 || v == 10) run<52>("pipelined_terms_stamps", g, nwg, false);
   return 0;
 }

@@ -219,6 +219,31 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
           }
     uint4* st = sm.stage[wave];
     _Float16* P = reinterpret_cast<_Float16*>(op.planes);
+    if (op.pad2 == 1) {
+      // development variant (TQ_S2D_PSTAGE=0): no LDS staging -- each lane stores its own four
+      // 16-B runs per plane (a store instruction: 32 rows x 32 contiguous bytes)
+      const int64_t rb = gbase + ooff[rt + fr] + 8 * fk;
+#pragma unroll
+      for (int pl = 0; pl < 6; ++pl)
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int e0 = 8 * h + 2 * j;
+              const f2v re = {d[tl][0][e0], d[tl][0][e0 + 1]}, im = {d[tl][1][e0], d[tl][1][e0 + 1]};
+              f2v t;
+              if (pl < 2) t = f16_terms(re, psc);
+              else if (pl < 4) t = f16_terms(im, psc);
+              else t = f16_terms(re + im, psc - 1);
+              w4[j] = __float_as_uint((pl & 1) ? t.y : t.x);
+            }
+            *reinterpret_cast<uint4*>(P + pl * op.pstride + rb + 32 * tl + 16 * h) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          }
+      return;
+    }
     const int row_w = fr;                       // this lane's row in the image (write side)
     const int row_r = lane >> 3, pc_r = lane & 7;   // read side: 8 lanes per row
     int64_t so[4];
@@ -441,6 +466,10 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     const char* e = getenv("TQ_S2D_DIAG");
     return e ? atoi(e) : 0;
   }();
+  static const bool pstage = [] {
+    const char* e = getenv("TQ_S2D_PSTAGE");
+    return !(e && e[0] == '0');
+  }();
   int blocks = 0;
   for (int q = 0; q < R.nops; ++q) {
     const int want = std::max(1, slots / R.nops);
@@ -448,6 +477,7 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     R.op[q].block_begin = blocks;
     R.op[q].pad = diag;
     R.op[q].order = order;
+    R.op[q].pad2 = pstage ? 0 : 1;
     blocks += R.op[q].nblocks;
   }
   hipLaunchKernelGGL(reinterpret_cast<void (*)(S2DLaunch)>(const_cast<void*>(fn)), dim3(blocks), dim3(64 * kWaves), 0,

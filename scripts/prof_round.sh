@@ -6,7 +6,7 @@ TAG=${1:-r04}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/p$TAG
 O=gpurun_out/p$TAG
 B="python3 bench.py --no-cpu-baseline --no-c5 --no-alt --no-other --steps 2 --warmup 1"
-R="--kernel-include-regex split_kernel|sweepd_kernel|sweep2_kernel --output-format csv"
+R="--kernel-include-regex split_kernel|gemm_planes_kernel|sweepd_kernel|sweep2_kernel --output-format csv"
 timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --no-cpu-baseline --no-c5 --no-alt --no-other > $O/kt.json 2> $O/kt.log || exit 1
 timeout -s KILL 90 rocprofv3 --kernel-trace $R -d $O/k0 -o run -- $B > $O/k0.log 2>&1 || exit 2
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT $R -d $O/p1 -o run -- $B > $O/p1.log 2>&1 || exit 3

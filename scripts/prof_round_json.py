@@ -10,7 +10,8 @@ import collections, csv, json, os, shutil, sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/p04"
 TAG = sys.argv[2] if len(sys.argv) > 2 else "r04"
-FAM = {"gemm_f16_split": "split_kernel", "dense_sweep": "sweepd_kernel", "sweep2": "sweep2_kernel"}
+FAM = {"gemm_f16_split": "split_kernel", "gemm_planes": "gemm_planes_kernel", "dense_sweep": "sweepd_kernel",
+       "sweep2": "sweep2_kernel"}
 
 
 def fam_of(name):
@@ -45,7 +46,7 @@ trace = dispatches(f"{root}/k0/run_kernel_trace.csv", value_col=False)
 passes = [dispatches(f"{root}/p{i}/run_counter_collection.csv") for i in (1, 2, 3, 4)]
 res = {"config": "C4",
        "command": f"scripts/prof_round.sh {TAG}: rocprofv3 --pmc <set> --kernel-include-regex "
-                  "'split_kernel|sweepd_kernel|sweep2_kernel' -- python3 bench.py --no-cpu-baseline --no-c5 "
+                  "'split_kernel|gemm_planes_kernel|sweepd_kernel|sweep2_kernel' -- python3 bench.py --no-cpu-baseline --no-c5 "
                   "--no-alt --steps 2 --warmup 1 (4 counter passes + a kernel-trace pass of the same command)",
        "definitions": {
            "hbm_bytes": "2*FETCH_SIZE + WRITE_SIZE (kB x 1024; gfx950 FETCH_SIZE correction)",
@@ -113,6 +114,37 @@ if gg:
            "definition": res["definitions"]["mfma_busy_frac"] + "; " + res["definitions"]["hbm_bytes"]
                          + "; algorithmic bytes = batch x (A + B once + C written)"}
     json.dump(gem, open(f"profiles/pmc_gemm_f16_{TAG}.json", "w"), indent=1)
+# the pre-split boundary GEMM (tq_gemmp.hip, default since r05) in the same schema
+gp = [g for g in res["groups"] if g["family"] == "gemm_planes"]
+if gp:
+    g = max(gp, key=lambda x: x["dispatches"])
+    batch, M, N, K = 4, 1024, 1024, 65536
+    n_mfma = batch * 3 * 3 * (M // 16) * (N // 16) * (K // 32)   # v_mfma_f32_16x16x32_f16
+    c = g["counters_avg"]
+    gem = {"config": "C4",
+           "kernel": ("gemm_planes_kernel (complex64 from six f16 term planes per operand stored by the dense "
+                      "producers; Gauss 3M x 3 term products on v_mfma_f32_16x16x32_f16, 256x256 tiles, "
+                      "LDS-DMA staged planes, M=N=1024, K=65536 per slice, batch 4 (slice lanes), split-K 4)"),
+           "command": res["command"],
+           "launches": g["dispatches"],
+           "counters_avg_per_launch": c,
+           "expected_mfma_per_launch": n_mfma,
+           "busy_cycles_per_mfma": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / n_mfma,
+           "avg_launch_ns_trace": g["avg_ns"],
+           "effective_clock_GHz": g.get("effective_clock_GHz"),
+           "mfma_busy_frac": g.get("mfma_busy_frac"),
+           "wait_frac": g.get("wait_frac"),
+           "wait_lds_frac": g.get("wait_lds_frac"),
+           "FETCH_SIZE_kB_per_launch": c.get("FETCH_SIZE"),
+           "WRITE_SIZE_kB_per_launch": c.get("WRITE_SIZE"),
+           "hbm_bytes_per_launch": g.get("hbm_bytes"),
+           "batch": batch, "splits": 4,
+           "algorithmic_bytes_per_launch": batch * ((M * K + N * K) * 8 + M * N * 8),
+           "plane_bytes_per_launch": batch * (M * K + N * K) * 12,
+           "definition": res["definitions"]["mfma_busy_frac"] + "; " + res["definitions"]["hbm_bytes"]
+                         + "; algorithmic bytes = batch x (complex64 A + B once + C written); the planes are "
+                           "12 B per operand element (1.5x the complex64 bytes)"}
+    json.dump(gem, open(f"profiles/pmc_gemm_planes_{TAG}.json", "w"), indent=1)
 st = f"{root}/kt/run_kernel_stats.csv"
 if os.path.exists(st):
     shutil.copy(st, f"profiles/rocprof_{TAG}_bench_kernel_stats.csv")
