@@ -2986,6 +2986,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
             o.tout = op.tout;
             o.block_begin = blocks;
             o.nblocks = s2d_blocks(op.ncols);
+            o.ncols = op.ncols;
             blocks += o.nblocks;
             o.beta = op.writes_output ? beta_out : 0.0;
             o.use_beta = o.beta != 0.0;

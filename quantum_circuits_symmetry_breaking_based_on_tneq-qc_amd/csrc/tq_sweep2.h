@@ -201,6 +201,7 @@ struct S2DOp {
   uint32_t* amax = nullptr;        // as S2Op::amax
   const int32_t* split_sc = nullptr;  // as S2Op::split_sc
   int order = 0, pad2 = 0;         // tile order (tq_sweepd.hip): 0 grid-strided, 1 blocked
+  int64_t ncols = 0;               // host copy (the launcher shares the workgroups by work)
   // planes mode (the pre-split boundary GEMM, tq_gemmp.hip): Y is not written; instead the six f16
   // term planes (re_h, re_l, im_h, im_l, s_h, s_l) of Y * 2^sc go to planes + p * pstride (element
   // offsets as Y's), sc from the bound max|Y| <= sqrt(2) max(|re X|, |im X|) max_r sum_k |M[r][k]|

@@ -51,6 +51,16 @@ __device__ __forceinline__ cst<T>* as_const(const void* p) {
 
 // f16 terms of v * 2^sc (S2DOp::split_sc; the consuming GEMM's pre-split operand form, as
 // tq_sweep2.hip's f16_terms)
+// f16 terms (h, l) of two values already scaled: h = f16(x), l = f16(x - h)
+__device__ __forceinline__ f2v f16_terms_scaled(f2v v) {
+  const f16x2 hv = {(_Float16)v.x, (_Float16)v.y};
+  const uint32_t h = __builtin_bit_cast(uint32_t, hv);
+  float r0, r1;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r0) : "v"(v.x), "v"(h));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r1) : "v"(v.y), "v"(h));
+  const f16x2 lv = {(_Float16)r0, (_Float16)r1};
+  return f2v{__uint_as_float(h), __uint_as_float(__builtin_bit_cast(uint32_t, lv))};
+}
 __device__ __forceinline__ f2v f16_terms(f2v v, int sc) {
   const float x0 = ldexpf(v.x, sc), x1 = ldexpf(v.y, sc);
   const f16x2 hv = {(_Float16)x0, (_Float16)x1};
@@ -74,9 +84,6 @@ template <int TMAX>
 struct SdSmem {
   float mp[2][TMAX * kS2DMaxTout];
   float red[kWaves];
-  // planes mode: a wave's [32 rows][8 x 16-B pieces] image of one plane (pieces XOR-swizzled by
-  // row), so that every store instruction writes 8 whole 128-byte row segments
-  uint4 stage[kWaves][32 * 8];
   int32_t ooff[kS2DMaxTout];
   int64_t btab[2][kLevels][64];
   int64_t wcol[2][kS2MaxColBits];
@@ -110,7 +117,7 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
   // planes mode: the operand scale from an a-priori bound of the output, identical in every
   // workgroup of the op (so every lane of the operand is scaled alike)
   const bool planes = op.planes != nullptr;
-  int psc = 0;
+  int psc = 0, xsc = 0;
   if (planes) {
     float rs = 0.f;
     for (int r = tid; r < tout; r += 64 * kWaves) {
@@ -135,6 +142,18 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
       psc = 14 - e;   // bound * 2^psc in [2^14, 2^15): no f16 overflow (65504)
     }
     if (blockIdx.x == (unsigned)op.block_begin && tid == 0) *op.sc_out = psc;
+    // the scale is applied to the operands instead of every output: X by 2^xsc (its max to
+    // [1, 2), exact) as it is loaded, M by 2^(psc - xsc) here (exact: |M 2^(psc - xsc)| <=
+    // 2^16 by the bound), so the products come out scaled
+    const uint32_t xb = *op.amax_in;
+    const int XE = (int)((xb >> 23) & 0xff);
+    xsc = (xb == 0 || XE == 255) ? 0 : -(XE ? XE - 127 : (31 - __clz((int)(xb & 0x7fffff))) - 149);
+    __syncthreads();   // every wave has read M for the bound
+    for (int i = tid; i < tout * TIN; i += 64 * kWaves) {
+      mp[0][i] = ldexpf(mp[0][i], psc - xsc);
+      mp[1][i] = ldexpf(mp[1][i], psc - xsc);
+    }
+    __syncthreads();
   }
   // btab[io][l][v] = sum of the weights of the set bits of v among column bits 6+6l .. 6+6l+5
   for (int i = tid; i < 2 * kLevels * 64; i += 64 * kWaves) {
@@ -200,9 +219,11 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
   // planes mode: per wave a 64-column group (both 32-column tiles of a column-bit-5 pair) and 32
   // output rows at a time, computed transposed (D^T[c][r]: lane = row rt + (lane & 31), registers =
   // columns (e & 3) + 8 (e >> 2) + 4 fk); a permlane32 swap per register pair leaves every lane two
-  // runs of 8 consecutive columns per tile; per plane the four 16-B runs of a lane go to the wave's
-  // LDS image and come back so that 8 lanes hold one row's 128 B: each store instruction writes
-  // 8 whole 128-byte lines of the plane (the rows' 64-element runs are contiguous and aligned)
+  // runs of 8 consecutive columns per tile, split into the six f16 planes and stored 16 B per
+  // plane and run.  The dense op's output rows are consecutive 64-element runs of the operand
+  // (out_off = 64 r), so a wave's 32 x 64 tile is 4 KiB of each plane, written whole by the 4
+  // store instructions of that plane (both column tiles' runs are emitted per plane: writing one
+  // tile's halves of all rows first left half-written lines and ran 2.5x slower)
   auto emit_planes = [&](f32x16 (&d)[2][2], int64_t gbase, int rt) {
 #pragma unroll
     for (int tl = 0; tl < 2; ++tl)
@@ -217,11 +238,12 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
             d[tl][ri][a] = __uint_as_float(sw[0]);
             d[tl][ri][b] = __uint_as_float(sw[1]);
           }
-    uint4* st = sm.stage[wave];
     _Float16* P = reinterpret_cast<_Float16*>(op.planes);
-    if (op.pad2 == 1) {
-      // development variant (TQ_S2D_PSTAGE=0): no LDS staging -- each lane stores its own four
-      // 16-B runs per plane (a store instruction: 32 rows x 32 contiguous bytes)
+    {
+      // each lane stores its own four 16-B runs per plane: a store instruction covers 32 rows x
+      // 32 contiguous bytes, and the plane's 4 instructions fill the wave's 4 KiB (32 rows x
+      // 128 B) of that plane back to back (an LDS-staged form storing 8 whole rows per
+      // instruction measured the same)
       const int64_t rb = gbase + ooff[rt + fr] + 8 * fk;
 #pragma unroll
       for (int pl = 0; pl < 6; ++pl)
@@ -235,51 +257,18 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
               const int e0 = 8 * h + 2 * j;
               const f2v re = {d[tl][0][e0], d[tl][0][e0 + 1]}, im = {d[tl][1][e0], d[tl][1][e0 + 1]};
               f2v t;
-              if (pl < 2) t = f16_terms(re, psc);
-              else if (pl < 4) t = f16_terms(im, psc);
-              else t = f16_terms(re + im, psc - 1);
+              if (pl < 2) t = f16_terms_scaled(re);
+              else if (pl < 4) t = f16_terms_scaled(im);
+              else t = f16_terms_scaled((re + im) * 0.5f);   // one binade lower (exact)
               w4[j] = __float_as_uint((pl & 1) ? t.y : t.x);
             }
-            *reinterpret_cast<uint4*>(P + pl * op.pstride + rb + 32 * tl + 16 * h) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4* dst = reinterpret_cast<u32x4*>(P + pl * op.pstride + rb + 32 * tl + 16 * h);
+            const u32x4 v = {w4[0], w4[1], w4[2], w4[3]};
+            if constexpr (NTS) __builtin_nontemporal_store(v, dst);
+            else if (op.pad != 2) *dst = v;
+            else if (w4[0] == 12345u) *dst = v;   // development diagnostic TQ_S2D_DIAG=2: no stores
           }
-      return;
-    }
-    const int row_w = fr;                       // this lane's row in the image (write side)
-    const int row_r = lane >> 3, pc_r = lane & 7;   // read side: 8 lanes per row
-    int64_t so[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) so[q] = gbase + ooff[rt + 8 * q + row_r] + 8 * pc_r;
-#pragma unroll
-    for (int pl = 0; pl < 6; ++pl) {
-      // the lane's 4 pieces of this plane: tile tl, run h -> piece 4 tl + 2 h + fk (columns 8 x piece)
-#pragma unroll
-      for (int tl = 0; tl < 2; ++tl)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          uint32_t w4[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int e0 = 8 * h + 2 * j;
-            const f2v re = {d[tl][0][e0], d[tl][0][e0 + 1]}, im = {d[tl][1][e0], d[tl][1][e0 + 1]};
-            f2v t;
-            if (pl < 2) t = f16_terms(re, psc);
-            else if (pl < 4) t = f16_terms(im, psc);
-            else t = f16_terms(re + im, psc - 1);
-            w4[j] = __float_as_uint((pl & 1) ? t.y : t.x);
-          }
-          const int pc = 4 * tl + 2 * h + fk;
-          st[row_w * 8 + (pc ^ (row_w & 7))] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        }
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's image is complete (wave-private)
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 8 * q + row_r;
-        const uint4 v = st[r * 8 + (pc_r ^ (r & 7))];
-        *reinterpret_cast<uint4*>(P + pl * op.pstride + so[q]) = v;
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // reads done before the next plane's writes
-      __builtin_amdgcn_wave_barrier();
     }
   };
   // tile order: grid-strided (default: concurrently running workgroups write neighbouring 1-KiB
@@ -305,8 +294,8 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           const f2v v = X[bi + io[s] + 32 * tl + fr];
-          xr[tl][s] = v.x;
-          xi[tl][s] = v.y;
+          xr[tl][s] = ldexpf(v.x, xsc);
+          xi[tl][s] = ldexpf(v.y, xsc);
         }
       const int64_t gb = base(1, g);
       for (int rt = 0; rt < tout; rt += 32) {
@@ -466,18 +455,21 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     const char* e = getenv("TQ_S2D_DIAG");
     return e ? atoi(e) : 0;
   }();
-  static const bool pstage = [] {
-    const char* e = getenv("TQ_S2D_PSTAGE");
-    return !(e && e[0] == '0');
-  }();
+
+  // the round of resident workgroups shared by the ops in proportion to their work: every op
+  // stores the same bytes per output element, and its MFMA work grows with tin (C4's tin-16
+  // left op has twice the products of the tin-8 right op per element)
+  double wsum = 0;
+  for (int q = 0; q < R.nops; ++q)
+    wsum += (double)std::max<int64_t>(R.op[q].ncols, 1) * R.op[q].tout * (8.0 + R.op[q].tin);
   int blocks = 0;
   for (int q = 0; q < R.nops; ++q) {
-    const int want = std::max(1, slots / R.nops);
+    const double wq = (double)std::max<int64_t>(R.op[q].ncols, 1) * R.op[q].tout * (8.0 + R.op[q].tin);
+    const int want = std::max(1, (int)((double)slots * wq / wsum));
     R.op[q].nblocks = std::max(1, std::min(R.op[q].nblocks, want));
     R.op[q].block_begin = blocks;
     R.op[q].pad = diag;
     R.op[q].order = order;
-    R.op[q].pad2 = pstage ? 0 : 1;
     blocks += R.op[q].nblocks;
   }
   hipLaunchKernelGGL(reinterpret_cast<void (*)(S2DLaunch)>(const_cast<void*>(fn)), dim3(blocks), dim3(64 * kWaves), 0,
