@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(NT) gemm3(Args g) {
     const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(f16x8, v);
   };
-  unsigned long long t0 = 0, r0 = 0;
+  unsigned long long t0 = 0, r0 = 0, wait_cyc = 0;
   if constexpr (VAR & 16) {
     if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
   }
@@ -310,12 +310,26 @@ __global__ void __launch_bounds__(NT) gemm3(Args g) {
     // the MFMAs stay above the wait: hipcc would otherwise hoist the wait for the NEXT step's
     // DMA in front of them and expose its latency every step
     if constexpr (!(VAR & 8)) __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    unsigned long long tw0 = 0;
+    if constexpr ((VAR & 128) != 0) {
+      if (tid == 0) tw0 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr ((VAR & 128) != 0) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (tid == 0) wait_cyc += __builtin_amdgcn_s_memtime() - tw0;   // own DMA + reads only
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
   }
   if constexpr (VAR & 16) {
     if (tid == 0) {
       unsigned long long* st = g.stamps + 4 * blockIdx.x;
       st[0] = t0; st[1] = r0; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+      if constexpr ((VAR & 128) != 0) st[1] = wait_cyc, st[3] = st[2] - t0;   // (loop cycles, wait cycles)
     }
   }
   float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
@@ -429,8 +443,10 @@ __global__ void __launch_bounds__(NT) gemm4(Args g) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) A[i] = rd(lds, aoff(i));
   auto step = [&](int t, f16x8 (&BH)[4], f16x8 (&BL)[4]) {
-    const char* s = lds + (t & 1) * 4 * TB3;
-    const char* sn = lds + ((t & 1) ^ 1) * 4 * TB3;
+    int so = (t & 1) * 4 * TB3, sno = ((t & 1) ^ 1) * 4 * TB3;
+    asm volatile("" : "+v"(so), "+v"(sno));   // opaque: no per-buffer address register sets
+    const char* s = lds + so;
+    const char* sn = lds + sno;
     if (t + 1 < nk) stage(t + 1, (t & 1) ^ 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) BL[j] = rd(s, boff(j) + TB3);
@@ -480,9 +496,303 @@ __global__ void __launch_bounds__(NT) gemm4(Args g) {
       }
 }
 
+// VAR & 64 (gemm5): 256 x 128 tiles, 8 waves (4 over M x 2 over N) of 64 x 64, THREE LDS stages
+// of 48 KiB (Ah, Al 16 KiB; Bh, Bl 8 KiB) so the LDS-DMA of step t + 2 flies while step t computes
+// (prefetch distance 2, counted vmcnt), and two fragment register sets: the barrier sits before
+// the third term product, after which the next step's fragments are read under its MFMAs
+constexpr int BN5 = 128, TA5 = BK3 * BM * 2, TB5 = BK3 * BN5 * 2, ST5 = 2 * TA5 + 2 * TB5;
+template <int VAR>
+__global__ void __launch_bounds__(NT) gemm5(Args g) {
+  __shared__ __attribute__((aligned(1024))) char lds[3 * ST5];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 3, wn = w >> 2;
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int nt = g.N / BN5, ntile = (g.M / BM) * nt;
+  const int tile = L % ntile, grp = L / ntile;
+  const int split = grp % g.splits, b = grp / g.splits;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN5;
+  const long long K1 = g.K / 3;
+  const long long k0 = split * (K1 / g.splits);
+  const int nk = (int)(K1 / g.splits / BK3);
+  const int lane_i = b / 3, prod = b % 3;
+  const long long psA = K1 * g.M, psB = K1 * g.N;
+  const _Float16* Ah = g.A + (long long)lane_i * 6 * psA + (2 * prod) * psA + k0 * g.M + m0;
+  const _Float16* Bh = g.B + (long long)lane_i * 6 * psB + (2 * prod) * psB + k0 * g.N + n0;
+  // A image: rows of 512 B (16 chunks of 32 B), 2 wave-instructions per plane per wave (rows
+  // 2 (8 i + w) + lane / 32); B image: rows of 256 B (8 chunks), 1 wave-instruction per plane per
+  // wave (rows 4 w + lane / 16)
+  uint32_t goA[2], goB;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 2 * (8 * i + w) + (lane >> 5);
+    const int c = ((lane & 31) >> 1) ^ fsw(r);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8) * 2;
+  }
+  {
+    const int r = 4 * w + (lane >> 4);
+    const int c = ((lane & 15) >> 1) ^ fsw(r);
+    goB = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8) * 2;
+  }
+  const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
+  auto glds16 = [&](const _Float16* base, uint32_t voff, unsigned off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(base), "s"(dst) : "memory");
+  };
+  auto stage = [&](int t) {   // 6 LDS-DMA instructions per thread
+    const _Float16* pa = Ah + (long long)t * BK3 * g.M;
+    const _Float16* pb = Bh + (long long)t * BK3 * g.N;
+    const unsigned o = (unsigned)(t % 3) * ST5;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16(pa, goA[i], o + (8 * i + w) * 1024);
+      glds16(pa + psA, goA[i], o + TA5 + (8 * i + w) * 1024);
+    }
+    glds16(pb, goB, o + 2 * TA5 + w * 1024);
+    glds16(pb + psB, goB, o + 2 * TA5 + TB5 + w * 1024);
+  };
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int x = q | ((g4 & 1) << 2);
+  const int rowa = (8 * g4 + q) * (BM * 2) + 8 * p, rowbb = (8 * g4 + q) * (BN5 * 2) + 8 * p;
+  int aoff[4], boff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) aoff[i] = rowa + ((wm * 4 + i) ^ x) * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) boff[j] = 2 * TA5 + rowbb + ((wn * 4 + j) ^ x) * 32;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto rdA = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BM * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto rdB = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BN5 * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  struct Frag { f16x8 ah[4], al[4], bh[4], bl[4]; };
+  auto read_all = [&](int t, Frag& f) {
+    // the stage offset as an opaque per-step value: hipcc would otherwise keep 3 x 16 address
+    // registers (one set per stage) live across the loop
+    int so = (t % 3) * ST5;
+    asm volatile("" : "+v"(so));
+    const char* s = lds + so;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.bh[j] = rdB(s, boff[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.ah[i] = rdA(s, aoff[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.bl[j] = rdB(s, boff[j] + TB5);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.al[i] = rdA(s, aoff[i] + TA5);
+  };
+  auto mm = [&](const f16x8 (&a)[4], const f16x8 (&bb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], bb[j], acc[i][j], 0, 0, 0);
+  };
+  unsigned long long t0 = 0, r0 = 0;
+  if constexpr (VAR & 16) {
+    if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  }
+  Frag F0, F1;
+  stage(0);
+  stage(1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // stage 0 landed (this wave)
+  __builtin_amdgcn_s_barrier();
+  read_all(0, F0);
+  // step t: the fragments of t are in `cur` (read under the previous step's last products)
+  auto step = [&](int t, Frag& cur, Frag& nxt) {
+    if (t + 2 < nk) stage(t + 2);           // into the stage step t - 1 used (free: its barrier)
+    mm(cur.ah, cur.bh);                      // h h
+    mm(cur.ah, cur.bl);                      // h l
+    __builtin_amdgcn_sched_barrier(0);
+    // stage t + 1 landed (this wave: all but the 6 just issued; none issued on the last two
+    // steps), this step's reads done; then for every wave
+    if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nk) read_all(t + 1, nxt);
+    mm(cur.al, cur.bh);                      // l h (under the next step's reads)
+  };
+  for (int t = 0; t < nk; t += 2) {   // nk even
+    step(t, F0, F1);
+    step(t + 1, F1, F0);
+  }
+  if constexpr (VAR & 16) {
+    if (tid == 0) {
+      unsigned long long* st = g.stamps + 4 * blockIdx.x;
+      st[0] = t0; st[1] = r0; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + g4 * 4 + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        C[(long long)m * g.N + n] = acc[i][j][r];
+      }
+}
+
+template <int VAR>
+__global__ void __launch_bounds__(NT) gemm6(Args g) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 4 * TB3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int nt = g.N / BN, ntile = (g.M / BM) * nt;
+  const int tile = L % ntile, grp = L / ntile;
+  const int split = grp % g.splits, b = grp / g.splits;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
+  const long long K1 = g.K / 3;            // k per term plane
+  const long long k0 = split * (K1 / g.splits);
+  const int nk = (int)(K1 / g.splits / BK3);
+  const int lane_i = b / 3, prod = b % 3;
+  const long long psA = K1 * g.M, psB = K1 * g.N;   // plane strides
+  const _Float16* Ah = g.A + (long long)lane_i * 6 * psA + (2 * prod) * psA + k0 * g.M + m0;
+  const _Float16* Bh = g.B + (long long)lane_i * 6 * psB + (2 * prod) * psB + k0 * g.N + n0;
+  uint32_t goA[2], goB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 2 * (8 * i + w) + (lane >> 5);
+    const int c = ((lane & 31) >> 1) ^ fsw(r);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8) * 2;   // bytes
+    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8) * 2;
+  }
+  const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
+  // SGPR base + 32-bit lane byte offset (global_load_lds_dwordx4 v, s[]): no 64-bit address VGPRs
+  auto glds16 = [&](const _Float16* base, uint32_t voff, unsigned off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(base), "s"(dst) : "memory");
+  };
+  auto stage = [&](int t, int buf) {
+    const _Float16* pa = Ah + (long long)t * BK3 * g.M;
+    const _Float16* pb = Bh + (long long)t * BK3 * g.N;
+    const unsigned o = buf * 4 * TB3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16(pa, goA[i], o + (8 * i + w) * 1024);
+      glds16(pa + psA, goA[i], o + TB3 + (8 * i + w) * 1024);
+      glds16(pb, goB[i], o + 2 * TB3 + (8 * i + w) * 1024);
+      glds16(pb + psB, goB[i], o + 3 * TB3 + (8 * i + w) * 1024);
+    }
+  };
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int x = q | ((g4 & 1) << 2);
+  const int rowb = (8 * g4 + q) * (BM * 2) + 8 * p;
+  int aoff[8], boff[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) aoff[i] = rowb + ((wm * 8 + i) ^ x) * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) boff[j] = 2 * TB3 + rowb + ((wn * 4 + j) ^ x) * 32;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto rd = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BM * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+  };
+  unsigned long long t0 = 0, r0 = 0, wait_cyc = 0;
+  if constexpr (VAR & 16) {
+    if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  }
+  // ping-pong: waves 4..7 (the second wave of every SIMD) run one phase behind waves 0..3, so
+  // on each SIMD one wave multiplies while its partner reads its next fragments.  Phases
+  // alternate R (fragment reads of step t) and M (its 96 MFMAs), one barrier after each.  The
+  // DMA of stage s is issued by both groups in interval 2s - 2 (group A in its R(s - 1), group B
+  // in its M(s - 2)) into the buffer whose readers all passed barrier 2s - 2, and each group
+  // waits for its own part at the end of the phase that precedes barrier 2s
+  const bool gb = __builtin_amdgcn_readfirstlane(w) >= 4;
+  f16x8 ah[8], al[8], bh[4], bl[4];
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (gb) {
+    if (nk > 1) stage(1, 1);
+    __builtin_amdgcn_s_barrier();            // the offset: group B one interval behind
+  }
+  for (int t = 0; t < nk; ++t) {
+    const char* s = lds + (t & 1) * 4 * TB3;
+    // ---- R(t)
+    if (!gb && t + 1 < nk) stage(t + 1, (t & 1) ^ 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bh[j] = rd(s, boff[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ah[i] = rd(s, aoff[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bl[j] = rd(s, boff[j] + TB3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) al[i] = rd(s, aoff[i] + TB3);
+    if (gb) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- M(t)
+    if (gb && t + 2 < nk) stage(t + 2, t & 1);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (gb) asm volatile("s_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (!gb) __builtin_amdgcn_s_barrier();     // the barrier count of group B's offset
+  if constexpr (VAR & 16) {
+    if (tid == 0) {
+      unsigned long long* st = g.stamps + 4 * blockIdx.x;
+      st[0] = t0; st[1] = r0; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+      if constexpr ((VAR & 128) != 0) st[1] = wait_cyc, st[3] = st[2] - t0;   // (loop cycles, wait cycles)
+    }
+  }
+  float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + i * 16 + g4 * 4 + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        C[(long long)m * g.N + n] = acc[i][j][r];
+      }
+}
+
 template <int VAR>
 static void launch(int nwg, const Args& g) {
-  if constexpr (VAR & 32) hipLaunchKernelGGL(gemm4<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  if constexpr (VAR & 256) hipLaunchKernelGGL(gemm6<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  else if constexpr (VAR & 64) hipLaunchKernelGGL(gemm5<VAR>, dim3(nwg * 2), dim3(NT), 0, 0, g);
+  else if constexpr (VAR & 32) hipLaunchKernelGGL(gemm4<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
   else if constexpr (VAR & 4) hipLaunchKernelGGL(gemm3<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
   else hipLaunchKernelGGL(gemm<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
 }
@@ -526,6 +836,12 @@ static void run(const char* name, Args g, int nwg, bool check) {
     }
     std::sort(c.begin(), c.end());
     if (!c.empty()) clk = c[c.size() / 2];
+    if (VAR & 128) {
+      double wsum = 0, lsum = 0;
+      for (int i = 0; i < nwg; ++i) { wsum += (double)st[4 * i + 1]; lsum += (double)st[4 * i + 3]; }
+      printf("{\"vmcnt_lgkm_wait_share\": %.4f}\n", wsum / lsum);
+      clk = 0;
+    }
   }
   double maxrel = -1;
   if (check) {
@@ -587,7 +903,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&A, na * 2));
   CK(hipMalloc(&B, nb * 2));
   CK(hipMalloc(&g.C, (size_t)g.batch * g.splits * g.M * g.N * 4));
-  CK(hipMalloc(&g.stamps, (size_t)nwg * 4 * 8));
+  CK(hipMalloc(&g.stamps, (size_t)nwg * 2 * 4 * 8));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, A, (uint64_t)na, 1u);
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, B, (uint64_t)nb, 2u);
   CK(hipDeviceSynchronize());
@@ -604,5 +920,11 @@ int main(int argc, char** argv) {
   if (v == 0 || v == 8) run<12>("fused_terms_planar_nosb", g, nwg, false);
   if (v == 0 || v == 9) run<36>("pipelined_terms", g, nwg, true);
   if (v == 0 || v == 10) run<52>("pipelined_terms_stamps", g, nwg, false);
+  if (v == 0 || v == 13) run<148>("fused_terms_waitstamps", g, nwg, false);
+  if (v == 0 || v == 14) run<260>("pingpong", g, nwg, true);
+  if (v == 0 || v == 15) run<276>("pingpong_stamps", g, nwg, false);
+  if (v == 0 || v == 16) run<261>("pingpong_setprio", g, nwg, false);
+  if (v == 0 || v == 11) run<68>("tile256x128_3stage", g, nwg, true);
+  if (v == 0 || v == 12) run<84>("tile256x128_3stage_stamps", g, nwg, false);
   return 0;
 }
