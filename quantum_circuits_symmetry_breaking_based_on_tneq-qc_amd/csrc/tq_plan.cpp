@@ -1626,7 +1626,109 @@ class Compiler {
     };
     choose(ld);
     choose(st);
-    for (int p = 0; p < kS2MaxPos; ++p) d.vsw[p] = vsw[p] < 0 ? 0 : vsw[p];
+    // ---- LDS bank model.  The tile image of (position set p, column c) is
+    //   ((p << logC) | c) ^ S(p),  S(p) = XOR of vsw[q] over the positions q in p,
+    // vsw[q] a 5-bit vector: only address bits below 5 are XOR-ed, so the map is a bijection of
+    // the tile when the images of the address bits below 5 stay independent (columns j: 1 << j,
+    // positions q with q + logC < 5: (1 << (q + logC)) ^ vsw[q]; s2_swz_valid).
+    // A wave's LDS access is served in lane groups (MI355X_MICROARCH.md §LDS; 8-byte elements:
+    // ds_read_b64 2 x 32 lanes on element mod 32, ds_write_b64 4 x 16 lanes on element mod 16);
+    // every access of the kernel is XOR-linear in its lane bits, so a group of 2^k lanes whose
+    // address differences span k directions with bank effects of rank r is 2^(k - r)-way.  The
+    // lane directions: the load (LDS writes) and store (reads) enumerations, and for every pass
+    // the columns then the pass positions (tq_sweep2.hip gate_pass_u / block_pass group index).
+    // Chunks of fewer than 32 columns put pass positions into the lane groups, which a swizzle
+    // of the column bits alone (r04) could not separate: the r04 PMC's 0.9 conflict cycles per
+    // sweep2 LDS instruction on C4's 8-column slice ops.  The vectors: the enumerations' choice,
+    // then a coordinate descent on the modeled cost (0 on every sweep op of C2 / C3 / C4).
+    int swl[kS2MaxPos], rl, rm, wl, wm;   // log2 lanes per group / log2 bank modulus (elements)
+    if (P_.esz <= 4) rl = rm = wl = wm = 5;
+    else if (P_.esz == 8) { rl = rm = 5; wl = wm = 4; }
+    else { rl = rm = 4; wl = wm = 3; }
+    {
+      struct Pat { std::vector<int> dirs; double rd, wr; };   // column j -> -(j + 1), position q -> q
+      std::vector<Pat> pats;
+      auto enum_dirs = [&](const std::vector<CBit>& e) {
+        std::vector<int> v;
+        for (size_t t = 0; t < e.size() && t < 5; ++t) v.push_back(e[t].col >= 0 ? -(e[t].col + 1) : e[t].pos);
+        return v;
+      };
+      pats.push_back({enum_dirs(ld), 0.0, double(int64_t(1) << d.nld)});
+      pats.push_back({enum_dirs(st), double(int64_t(1) << d.nst), 0.0});
+      const int ng = (int)c.gates.size() - (d.epi ? 1 : 0);   // as the pass loop below
+      for (int j = 0; j < ng;) {
+        uint32_t bm, lv, mask;
+        double rd, wr;
+        const int e = block_span(j, ng, &bm, &lv);
+        if (e - j < 2) mask = d.gate[j].pass_mask, rd = d.gate[j].K, wr = d.gate[j].N;
+        else mask = lv & ~bm, rd = wr = double(1 << B);
+        j = e - j < 2 ? j + 1 : e;
+        std::vector<int> v;
+        for (int q = 0; q < d.logC && v.size() < 5; ++q) v.push_back(-(q + 1));
+        for (uint32_t m = mask; m && v.size() < 5; m &= m - 1) v.push_back(__builtin_ctz(m));
+        const double groups = double(int64_t(1) << (d.logC + __builtin_popcount(mask)));
+        pats.push_back({v, groups * rd, groups * wr});
+      }
+      double ideal = 0;
+      for (auto& pt : pats) ideal += pt.rd / double(1 << rl) + pt.wr / double(1 << wl);
+      auto cost = [&](const int* w) {   // modeled extra LDS cycles per chunk
+        double x = 0;
+        for (auto& pt : pats)
+          for (int side = 0; side < 2; ++side) {
+            const double n = side ? pt.wr : pt.rd;
+            const int lg = side ? wl : rl, mb = (1 << (side ? wm : rm)) - 1;
+            if (n <= 0) continue;
+            std::vector<int> eff;
+            for (int t = 0; t < (int)pt.dirs.size() && t < lg; ++t) {
+              const int dd = pt.dirs[t];
+              eff.push_back((dd < 0 ? (1 << (-dd - 1)) : ((1 << (dd + d.logC)) ^ w[dd])) & mb);
+            }
+            const int k = (int)eff.size();
+            x += n * double((1 << (k - gf2_rank(eff))) - 1) / double(1 << lg);
+          }
+        return x;
+      };
+      const int cm = (1 << d.logC) - 1;
+      for (int q = 0; q < kS2MaxPos; ++q) swl[q] = (vsw[q] < 0 ? 0 : vsw[q]) & cm;   // the r04 layout
+      d.lds_model[0] = (float)(ideal > 0 ? cost(swl) / ideal : 0.0);
+      // start from the enumerations' choice, then coordinate descent over the eligible positions'
+      // vectors (strict improvements only: a conflict-free r04 layout stays as it was)
+      // positions that reach a lane group: the only ones whose vector matters
+      uint32_t rel = 0;
+      for (auto& pt : pats)
+        for (int dd : pt.dirs)
+          if (dd >= 0 && dd < used) rel |= 1u << dd;
+      const int lowb = std::min(5, d.logC + used);   // address bits the swizzle may write
+      auto valid = [&](const int* w) {
+        std::vector<int> im;
+        for (int b = 0; b < lowb; ++b) im.push_back(b < d.logC ? 1 << b : (1 << b) ^ w[b - d.logC]);
+        return gf2_rank(im) == lowb;
+      };
+      auto descend = [&](int* w) {
+        double b = cost(w);
+        for (int it = 0; it < 6 && b > 0; ++it) {
+          bool moved = false;
+          for (int q = 0; q < kS2MaxPos; ++q) {
+            if (!((rel >> q) & 1)) continue;
+            int bv = w[q];
+            for (int v = 0; v < (1 << lowb); ++v) {
+              if (v == bv) continue;
+              w[q] = v;
+              if (q + d.logC < 5 && !valid(w)) continue;
+              const double x = cost(w);
+              if (x < b - 1e-9) b = x, bv = v, moved = true;
+            }
+            w[q] = bv;
+          }
+          if (!moved) break;
+        }
+        return b;
+      };
+      for (int q = 0; q < kS2MaxPos; ++q) swl[q] = (vsw[q] < 0 || q + d.logC < 5) ? 0 : vsw[q];
+      double best = descend(swl);
+      d.lds_model[1] = (float)(ideal > 0 ? best / ideal : 0.0);
+    }
+    for (int p = 0; p < kS2MaxPos; ++p) d.vsw[p] = swl[p];
     auto code = [&](const CBit& b) {
       if (b.col >= 0) return 1 << b.col;
       return ((1 << b.pos) << kS2CodeP) | (d.vsw[b.pos] << kS2CodeS);
@@ -1639,11 +1741,11 @@ class Compiler {
     for (size_t t = 0; t < ld.size(); ++t) { d.ld_w[t] = ld[t].w; d.ld_code[t] = code(ld[t]); }
     for (size_t t = 0; t < st.size(); ++t) { d.st_w[t] = st[t].w; d.st_code[t] = code(st[t]); }
     if (!s2_lane_offsets_fit(d.ld_w, d.nld, d.st_w, d.nst, (int64_t)P_.esz)) return false;
-    // LDS element address of a code: (p << logC) + (c ^ (s & (C-1))) -- XOR-linear in the code
+    // LDS element address of a code: ((p << logC) | c) ^ s -- XOR-linear in the code
     auto lds_addr = [&](int cd) {
       const int p = (cd >> kS2CodeP) & ((1 << kS2MaxPos) - 1), cc = cd & ((1 << kS2CodeP) - 1),
                 sv = (cd >> kS2CodeS) & 31;
-      return (p << d.logC) + (cc ^ (sv & ((1 << d.logC) - 1)));
+      return ((p << d.logC) | cc) ^ sv;
     };
     for (int t = 0; t < d.nld; ++t) d.ld_a[t] = lds_addr(d.ld_code[t]);
     for (int t = 0; t < d.nst; ++t) d.st_a[t] = lds_addr(d.st_code[t]);
@@ -1662,18 +1764,17 @@ class Compiler {
       for (int p = 0; p < kS2MaxPos; ++p) if ((bits >> p) & 1) v ^= d.vsw[p];
       return v;
     };
-    const int cmask = (1 << d.logC) - 1;
     for (size_t j = 0; j < c.gates.size(); ++j) {
       S2Gate& G = d.gate[j];
       for (int k = 0; k < G.K; ++k) {
         G.kdep[k] = kdep[j][k];
         G.ksw[k] = swz(kdep[j][k]);
-        G.kaddr[k] = (G.kdep[k] << d.logC) ^ (G.ksw[k] & cmask);
+        G.kaddr[k] = (G.kdep[k] << d.logC) ^ G.ksw[k];
       }
       for (int n = 0; n < G.N; ++n) {
         G.ndep[n] = ndep[j][n];
         G.nsw[n] = swz(ndep[j][n]);
-        G.naddr[n] = (G.ndep[n] << d.logC) ^ (G.nsw[n] & cmask);
+        G.naddr[n] = (G.ndep[n] << d.logC) ^ G.nsw[n];
       }
     }
     // gate fields and group tables (what the kernel used to build per workgroup)
@@ -1695,7 +1796,7 @@ class Compiler {
           if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
           if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
         }
-        d.k.lut[j][jj] = ((base << d.logC) ^ (sw & cmask)) * (int32_t)P_.esz;   // bytes
+        d.k.lut[j][jj] = ((base << d.logC) ^ sw) * (int32_t)P_.esz;   // bytes
       }
     }
     // passes: register blocks of consecutive square gates (S2Desc::pmeta), single gates otherwise
@@ -1712,7 +1813,7 @@ class Compiler {
             if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
             if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
           }
-          lut[jj] = ((base << d.logC) ^ (sw & cmask)) * (int32_t)P_.esz;   // bytes
+          lut[jj] = ((base << d.logC) ^ sw) * (int32_t)P_.esz;   // bytes
         }
       };
       int j = 0;
@@ -1741,7 +1842,7 @@ class Compiler {
         for (int q = 0; q < kS2MaxPos; ++q)
           if ((bm >> q) & 1) bp[nb++] = q;
         for (int b = 0; b < B; ++b)
-          pm[kS2PmAddr + b] = ((1 << bp[b]) << d.logC) ^ (d.vsw[bp[b]] & cmask);
+          pm[kS2PmAddr + b] = ((1 << bp[b]) << d.logC) ^ d.vsw[bp[b]];
         auto local = [&](int pos) {
           for (int b = 0; b < B; ++b) if (bp[b] == pos) return b;
           return -1;
@@ -1860,6 +1961,11 @@ class Compiler {
     for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
     o << " passes=" << d.npass;
     if (d.epi) o << " epi";
+    {
+      char b[48];
+      snprintf(b, sizeof b, " ldsx=%.2f->%.2f", d.lds_model[0], d.lds_model[1]);
+      o << b;
+    }
     op.note = o.str();
     P_.ops.push_back(op);
   }

@@ -41,7 +41,7 @@ struct S2Gate {
   int32_t kdep[kS2MaxKN] = {}, ndep[kS2MaxKN] = {};  // position bits of input k / output n
   int32_t ksw[kS2MaxKN] = {}, nsw[kS2MaxKN] = {};    // their swizzle contributions
   // LDS element-address XOR masks of input k / output n (linear in the position bits):
-  // (dep << logC) ^ (sw & (C-1))
+  // (dep << logC) ^ sw
   int32_t kaddr[kS2MaxKN] = {}, naddr[kS2MaxKN] = {};
   int32_t gidx[kS2MaxKN * kS2MaxKN] = {};             // coefficient k*N+n -> element of G
 };
@@ -96,6 +96,9 @@ struct S2Desc {
   int32_t ld_code[16] = {}, st_code[16] = {};
   int32_t ld_hc[kS2MaxSlots] = {}, st_hc[kS2MaxSlots] = {};
   int32_t vsw[12] = {};          // swizzle vector of each position (kS2MaxPos used)
+  // modeled extra LDS bank-conflict cycles / conflict-free cycles of a chunk: the r04 column-only
+  // swizzle, the chosen one (tq_plan.cpp s2_layout)
+  float lds_model[2] = {};
   alignas(8) S2Gate gate[kS2MaxGates];
 };
 constexpr int kS2KeepOff = (int)offsetof(S2Desc, k);

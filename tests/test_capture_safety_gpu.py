@@ -52,7 +52,8 @@ def test_drop_expression_inside_user_capture(dev):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         out = e_new(*x_new)
-        del e_old, e_grad          # last references (refcount): plans and runtime graphs die mid-capture
+        del e_old, e_grad          # last references: plans and runtime graphs die mid-capture,
+        gc.collect()               # by refcount or (a cycle through the runtime) by a collection
         parked = graphs.deferred_count()
     assert parked >= 2, parked       # at least one plan handle and the runtime's graph dict
     torch.cuda.synchronize()
