@@ -1238,6 +1238,14 @@ class Compiler {
   // narrowest chunk (log2 columns) of the small-tensor rule (TQ_S2_MINLC; 1 since r04: with the
   // 32-lane batches and 4096-element register-block tiles C2 0.399 -> 0.365 ms, C3 0.786 ->
   // 0.700, C4 N = 8 rank 2.21 -> 2.12, profiles/knobs_r04.jsonl; r03 measured 2 better alone)
+  // TQ_S2_SWZ=0: sweep2 tiles keep the r04 column-only swizzle instead of the modeled one
+  static bool s2_swz_model() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_SWZ");
+      return !(e && atoi(e) == 0);
+    }();
+    return v;
+  }
   static int s2_min_logc() {
     static const int v = [] {
       const char* e = getenv("TQ_S2_MINLC");
@@ -1724,8 +1732,13 @@ class Compiler {
         }
         return b;
       };
-      for (int q = 0; q < kS2MaxPos; ++q) swl[q] = (vsw[q] < 0 || q + d.logC < 5) ? 0 : vsw[q];
-      double best = descend(swl);
+      double best;
+      if (!s2_swz_model()) {   // TQ_S2_SWZ=0: the r04 column-only swizzle (A/B)
+        best = cost(swl);
+      } else {
+        for (int q = 0; q < kS2MaxPos; ++q) swl[q] = (vsw[q] < 0 || q + d.logC < 5) ? 0 : vsw[q];
+        best = descend(swl);
+      }
       d.lds_model[1] = (float)(ideal > 0 ? best / ideal : 0.0);
     }
     for (int p = 0; p < kS2MaxPos; ++p) d.vsw[p] = swl[p];
@@ -2692,6 +2705,15 @@ int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, 
                 int64_t s_step, int accumulate, hipStream_t stream) {
   if (P.profile || !P.use_graph || graphs_disabled())
     return plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, stream);
+  // a caller's stream capture (a torch.cuda.graph around the call): the launches go straight
+  // into that capture -- a graph of the plan's own, built on its side stream and launched into
+  // the capturing stream, ran once at capture time and was not part of the caller's replays
+  {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    TQ_HIP(hipStreamIsCapturing(stream, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      return plan_enqueue(P, inputs, out, s_begin, s_end, s_step, accumulate, stream);
+  }
   Plan::GraphKey key;
   key.inputs.assign(inputs, inputs + P.n_inputs);
   key.out = out; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
