@@ -151,7 +151,10 @@ int64_t tq_plan_query(tq_plan plan, const char* key);
  * "planes_active", "planes_bytes": the extra device memory), 0 on the GEMM-side split kernel;
  * "sweep_coop" = 0 (default, env TQ_S2_COOP) -- 1 runs consecutive hoisted levels of
  * multi-chunk sweep2 ops as one launch whose workgroups hand off through a counter barrier
- * (diagnostic: measured slower; a wait that gives up is counted in query "coop_timeouts"). */
+ * (diagnostic: measured slower).  Its workgroups must be co-resident: a wait that gives up
+ * (bounded spin) makes tq_plan_execute synchronize-check and fail with TQ_ERR_HIP ("the result
+ * is invalid") instead of returning the stale result; inside a caller's capture the check is
+ * skipped (query "coop_timeouts" then reports the count). */
 int tq_plan_set(tq_plan plan, const char* key, int64_t value);
 /* human-readable per-step description into buf (for debugging / DESIGN evidence) */
 int tq_plan_describe(tq_plan plan, char* buf, size_t n);

@@ -181,6 +181,7 @@ struct PlanesGemmArgs {
   int M = 0, N = 0, batch = 1, splits = 1;   // splits: set by the launcher
   int64_t K = 0;
   float* W = nullptr;                        // partials, planes_gemm_workspace bytes
+  size_t ws_bytes = 0;                       // capacity of W (the launcher refuses a launch beyond it)
 };
 // C + j sC (complex64, row stride ldc; one output when lane_sum) = [sum over batch entries j]
 // 2^-(sc_a[j stride] + sc_b[j stride]) x the complex product + beta C

@@ -27,6 +27,8 @@
 //     slice lanes (the plan's lane sum) in one pass.
 // Probe (probes/f16gemm_probe.hip, C4 shape, same executed flops as the split kernel's 5.1 ms):
 // 3.4-3.6 ms per 4-lane launch, 1.39-1.46 PF executed at 1.78-1.88 GHz.
+#include <algorithm>
+
 #include "tq_common.h"
 
 namespace tq {
@@ -238,8 +240,16 @@ bool planes_gemm_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
          ldb % 8 == 0 && (int64_t)kBK * lda < (int64_t(1) << 31) && (int64_t)kBK * ldb < (int64_t(1) << 31);
 }
 
-size_t planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch) {
+static size_t planes_ws_one(int64_t M, int64_t N, int64_t K, int64_t batch) {
   return (size_t)batch * 3 * planes_gemm_splits(M, N, K, batch) * M * N * sizeof(float);
+}
+
+// partials of a launch of up to `batch` entries: a partial lane batch (a slice range that is not a
+// multiple of the lanes) may pick more splits than a full one (C4, 4 lanes: 4 splits; 3: 16)
+size_t planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  size_t w = 0;
+  for (int64_t b = 1; b <= batch; ++b) w = std::max(w, planes_ws_one(M, N, K, b));
+  return w;
 }
 
 int planes_gemm_launch(const PlanesGemmArgs& a0, const PlanesCombineArgs& c0, hipStream_t stream) {
@@ -249,6 +259,10 @@ int planes_gemm_launch(const PlanesGemmArgs& a0, const PlanesCombineArgs& c0, hi
   }
   PlanesGemmArgs a = a0;
   a.splits = planes_gemm_splits(a.M, a.N, a.K, a.batch);
+  if (planes_ws_one(a.M, a.N, a.K, a.batch) > a.ws_bytes) {
+    set_error("planes gemm: partials exceed the workspace");
+    return TQ_ERR_INVALID;
+  }
   const int64_t nwg = (int64_t)a.batch * 3 * a.splits * (a.M / kBM) * (a.N / kBN);
   hipLaunchKernelGGL(gemm_planes_kernel, dim3((unsigned)nwg), dim3(kNT), 0, stream, a);
   TQ_HIP(hipGetLastError());

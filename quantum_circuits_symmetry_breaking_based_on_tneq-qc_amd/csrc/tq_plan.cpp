@@ -2678,6 +2678,31 @@ int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int
     P.run_mode = ok ? 1 : 0;
   }
   TQ_TRY(plan_launch(P, inputs, out, s_begin, s_end, s_step, accumulate, stream));
+  if (P.use_coop && !P.coop_once.empty() && P.d_tables) {
+    // cooperative chain launches (opt-in) rely on their workgroups being co-resident; a wait
+    // that gave up (sync[1], counted by the kernel) means the op read stale data: the execute
+    // synchronizes to check (outside a caller's capture) and fails instead of returning it
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    TQ_HIP(hipStreamIsCapturing(stream, &cs));
+    if (cs == hipStreamCaptureStatusNone) {
+      uint32_t gaveup = 0;
+      for (size_t r = 0; r < P.coop_once.size(); ++r) {
+        uint32_t w = 0;
+        char* slot = (char*)P.d_tables + P.sync_off + r * Plan::kSyncSlot + 4;
+        TQ_HIP(hipMemcpyAsync(&w, slot, 4, hipMemcpyDeviceToHost, stream));
+        TQ_HIP(hipStreamSynchronize(stream));
+        if (w) TQ_HIP(hipMemsetAsync(slot, 0, 4, stream));
+        gaveup += w;
+      }
+      if (gaveup) {
+        TQ_HIP(hipStreamSynchronize(stream));
+        set_error("cooperative sweep chain: " + std::to_string(gaveup) +
+                  " workgroup wait(s) gave up (workgroups not co-resident); the result is invalid -- "
+                  "run with sweep_coop 0");
+        return TQ_ERR_HIP;
+      }
+    }
+  }
   if (P.run_mode) {
     // slices whose operand max left its scale window produced zeros: add them on the split path
     const uint32_t* dbad = reinterpret_cast<const uint32_t*>((const char*)P.d_tables + P.bad_off);
@@ -2845,6 +2870,7 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
         a.K = op.K;
         a.batch = lane_gemm;
         a.W = reinterpret_cast<float*>((char*)P.d_planes + P.planes_ws_off);
+        a.ws_bytes = P.planes_sc_off - P.planes_ws_off;
         PlanesCombineArgs c;
         c.sc_a = planes_sc(j0, 0);
         c.sc_b = planes_sc(j0, 1);

@@ -225,6 +225,11 @@ def test_planes_gemm_equals_split_kernel(dev):
     _check(off, ref, TOL["complex64"], "split")
     assert np.abs(on - off).max() / np.abs(ref).max() < TOL["complex64"]
     assert np.array_equal(on, again)
+    # partial lane batches (3 + 5 slices over 4-lane batches): a launch of fewer entries than lanes
+    # may take more split-K partials than a full one (planes_gemm_workspace covers every size)
+    p1 = e(*ops, slice_range=(0, 3, 1)).cpu().numpy()
+    p2 = e(*ops, slice_range=(3, e.n_slices, 1)).cpu().numpy()
+    assert np.abs(p1 + p2 - on).max() / np.abs(ref).max() < TOL["complex64"]
 
 
 @pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 4)])
