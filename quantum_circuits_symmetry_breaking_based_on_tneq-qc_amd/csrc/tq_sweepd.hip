@@ -257,7 +257,8 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
               const int e0 = 8 * h + 2 * j;
               const f2v re = {d[tl][0][e0], d[tl][0][e0 + 1]}, im = {d[tl][1][e0], d[tl][1][e0 + 1]};
               f2v t;
-              if (pl < 2) t = f16_terms_scaled(re);
+              if (op.pad == 3) t = (pl & 2) ? im : re;   // development diagnostic: no split
+              else if (pl < 2) t = f16_terms_scaled(re);
               else if (pl < 4) t = f16_terms_scaled(im);
               else t = f16_terms_scaled((re + im) * 0.5f);   // one binade lower (exact)
               w4[j] = __float_as_uint((pl & 1) ? t.y : t.x);
@@ -307,6 +308,12 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
           for (int s = 0; s < KS; ++s) {
             const int a = (2 * s + fk) * tout + rt + fr;
             const float mr = mp[0][a], mi = mp[1][a];
+            if (op.pad == 1 || op.pad == 3) {   // development diagnostics: no MFMAs
+              p1[s] = xr[tl][s] * mr;
+              p2[s] = xi[tl][s] * mi;
+              p3[s] = mr + mi;
+              continue;
+            }
             p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[tl][s], mr, p1, 0, 0, 0);
             p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(xi[tl][s], mi, p2, 0, 0, 0);
             p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[tl][s] + xi[tl][s], mr + mi, p3, 0, 0, 0);

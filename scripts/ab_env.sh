@@ -11,7 +11,7 @@ for spec in "$@"; do
   python3 -c "
 import json
 d = json.loads([l for l in open('gpurun_out/abe_$label.log') if l.startswith('{')][-1])
-h = d['hbm_kernels']
-print('$label', round(d['ms_per_step'], 3), 'ms/step', round(d['value'] / 1e6, 2), 'M amp/s | gemm/step',
-      round(h['gemm_ms_per_step'], 3), 'sweep/step', round(h['sweep_ms_per_step'], 3), 'sweep GB/s', round(h['sweep_GBps']))"
+h = d.get('hbm_kernels') or {}
+print('$label', round(d['ms_per_step'], 4), 'ms/step', round(d['value'], 1), d['unit'], '| gemm/step',
+      h.get('gemm_ms_per_step'), 'sweep/step', h.get('sweep_ms_per_step'), 'sweep GB/s', h.get('sweep_GBps'))"
 done

@@ -260,40 +260,48 @@ def test_rccl_one_rank_all_reduce(dev):
 
 
 def _comm_engine_worker(rank, world, port, q):
-    """The reference trainer's construction (distributed_trainer.py:228-233, 271-283) on a
-    1-rank RCCL group: comm = get_comm_backend('torch') (CommTorch initialises the "nccl"
-    process group from the environment, device_id bound), DistributedEngineSiamese(backend=...,
-    strategy_mode=..., mx_K=..., comm=comm, partition_config=...) on the HIP backend, against
-    the single-process EngineSiamese; plus CommTorch's allreduce of a complex64 device tensor."""
+    """The reference trainer's construction (distributed_trainer.py:228-233, 271-283) on one GPU:
+    comm = get_comm_backend('torch'), then DistributedEngineSiamese(backend=..., strategy_mode=...,
+    mx_K=..., comm=comm, partition_config=...) on the HIP backend, against the single-process
+    EngineSiamese -- first as the trainer runs at world 1 (CommTorch, like comm_torch.py:140-175,
+    initialises no group there), then joining a 1-rank "nccl" (RCCL) group initialised as the
+    launcher / bench.py does, with CommTorch's allreduce of a complex64 device tensor over it."""
     import torch
+    import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
                       LOCAL_RANK="0")
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
+    from tneq_qc_amd.backends import BackendFactory
+    from tneq_qc_amd.core.engine_siamese import EngineSiamese
     from tneq_qc_amd.distributed import DistributedEngineSiamese, PartitionConfig, ReduceOp, get_comm_backend
-    comm = get_comm_backend("torch")
-    try:
-        from tneq_qc_amd.backends import BackendFactory
-        from tneq_qc_amd.core.engine_siamese import EngineSiamese
-        import torch.distributed as dist
-        be = dist.get_backend()
-        z = torch.randn(1 << 12, dtype=torch.complex64, device=dev)
-        e_ar = float((comm.allreduce(z, ReduceOp.SUM) - z).abs().max())
-        backend = BackendFactory.create_backend("hip", device="cuda:0", dtype="complex128")
-        qc, cores, states, mx = _engine_setup(dev)
-        ref = EngineSiamese(backend, "balanced").contract_with_compiled_strategy(qc, states, mx).cpu()
+    backend = BackendFactory.create_backend("hip", device="cuda:0", dtype="complex128")
+    qc, cores, states, mx = _engine_setup(dev)
+    ref = EngineSiamese(backend, "balanced").contract_with_compiled_strategy(qc, states, mx).cpu()
+
+    def run(comm):
         eng = DistributedEngineSiamese(backend=backend, strategy_mode="balanced", mx_K=100, comm=comm,
                                        partition_config=PartitionConfig(num_partitions=comm.world_size))
         same = eng.comm is comm and (eng.rank, eng.world_size) == (0, 1)
         eng.init_distributed(qc)
         res = eng.contract_distributed(states, mx).cpu()
-        e_fwd = float((res - ref).abs().max() / ref.abs().max())
+        return same, float((res - ref).abs().max() / ref.abs().max())
+
+    comm0 = get_comm_backend("torch")
+    local = (comm0.is_initialized(),) + run(comm0)
+    dist.init_process_group("nccl", device_id=dev)
+    comm = get_comm_backend("torch")
+    try:
+        z = torch.randn(1 << 12, dtype=torch.complex64, device=dev)
+        e_ar = float((comm.allreduce(z, ReduceOp.SUM) - z).abs().max())
+        rccl = (comm.is_initialized(), dist.get_backend()) + run(comm)
         comm.barrier()
-        q.put((rank, be, same, e_ar, e_fwd))
+        q.put((rank, local, rccl, e_ar))
     finally:
         comm.destroy()
 
 
 def test_reference_comm_engine_rccl_one_rank(dev):
-    (rank, be, same, e_ar, e_fwd), = _spawn(_comm_engine_worker, 1)
-    assert be == "nccl" and same and e_ar == 0.0 and e_fwd < 1e-12, (be, same, e_ar, e_fwd)
+    (rank, local, rccl, e_ar), = _spawn(_comm_engine_worker, 1)
+    assert local[0] is False and local[1] and local[2] < 1e-12, local
+    assert rccl[:3] == (True, "nccl", True) and rccl[3] < 1e-12 and e_ar == 0.0, (rccl, e_ar)
