@@ -72,6 +72,12 @@ __device__ __forceinline__ f2v f16_terms(f2v v, int sc) {
   return f2v{__uint_as_float(h), __uint_as_float(__builtin_bit_cast(uint32_t, lv))};
 }
 
+#ifndef TQ_S2D_DIAG
+// development diagnostics (a separate build, make EXTRA=-DTQ_S2D_DIAG=n): 1 no MFMAs, 2 no
+// stores, 3 no MFMAs and no f16 split (the planes path's store stream alone)
+#define TQ_S2D_DIAG 0
+#endif
+
 constexpr int kWaves = 4;             // waves per workgroup
 constexpr int kLevels = 7;            // column-base tables: 6 column bits each, bits 6 .. 47
 
@@ -211,9 +217,12 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
         const f2v a = f16_terms(f2v{w.x, w.y}, sc), b = f16_terms(f2v{w.z, w.w}, sc);
         w = f4v{a.x, a.y, b.x, b.y};
       }
+#if TQ_S2D_DIAG == 2
+      if (w.x == 12345.f) *p = w;   // development diagnostic: no stores
+#else
       if constexpr (NTS) __builtin_nontemporal_store(w, p);   // streaming stores (TQ_S2D_NT=1)
-      else if (op.pad != 2) *p = w;   // development diagnostic (TQ_S2D_DIAG=2): no stores
-      else if (w.x == 12345.f) *p = w;
+      else *p = w;
+#endif
     }
   };
   // planes mode: per wave a 64-column group (both 32-column tiles of a column-bit-5 pair) and 32
@@ -224,6 +233,10 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
   // (out_off = 64 r), so a wave's 32 x 64 tile is 4 KiB of each plane, written whole by the 4
   // store instructions of that plane (both column tiles' runs are emitted per plane: writing one
   // tile's halves of all rows first left half-written lines and ran 2.5x slower)
+  // the planes' base and stride as locals: read through `op` (the kernel-argument block, not
+  // provably unaliased by the stores) they were re-loaded by scalar loads inside the store loop
+  _Float16* const Pl = reinterpret_cast<_Float16*>(op.planes);
+  const int64_t pstride = op.pstride;
   auto emit_planes = [&](f32x16 (&d)[2][2], int64_t gbase, int rt) {
 #pragma unroll
     for (int tl = 0; tl < 2; ++tl)
@@ -238,7 +251,6 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
             d[tl][ri][a] = __uint_as_float(sw[0]);
             d[tl][ri][b] = __uint_as_float(sw[1]);
           }
-    _Float16* P = reinterpret_cast<_Float16*>(op.planes);
     {
       // each lane stores its own four 16-B runs per plane: a store instruction covers 32 rows x
       // 32 contiguous bytes, and the plane's 4 instructions fill the wave's 4 KiB (32 rows x
@@ -257,18 +269,24 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
               const int e0 = 8 * h + 2 * j;
               const f2v re = {d[tl][0][e0], d[tl][0][e0 + 1]}, im = {d[tl][1][e0], d[tl][1][e0 + 1]};
               f2v t;
-              if (op.pad == 3) t = (pl & 2) ? im : re;   // development diagnostic: no split
-              else if (pl < 2) t = f16_terms_scaled(re);
+#if TQ_S2D_DIAG == 3
+              t = (pl & 2) ? im : re;   // development diagnostic: no split
+#else
+              if (pl < 2) t = f16_terms_scaled(re);
               else if (pl < 4) t = f16_terms_scaled(im);
               else t = f16_terms_scaled((re + im) * 0.5f);   // one binade lower (exact)
+#endif
               w4[j] = __float_as_uint((pl & 1) ? t.y : t.x);
             }
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            u32x4* dst = reinterpret_cast<u32x4*>(P + pl * op.pstride + rb + 32 * tl + 16 * h);
+            u32x4* dst = reinterpret_cast<u32x4*>(Pl + pl * pstride + rb + 32 * tl + 16 * h);
             const u32x4 v = {w4[0], w4[1], w4[2], w4[3]};
+#if TQ_S2D_DIAG == 2
+            if (w4[0] == 12345u) *dst = v;   // development diagnostic: no stores
+#else
             if constexpr (NTS) __builtin_nontemporal_store(v, dst);
-            else if (op.pad != 2) *dst = v;
-            else if (w4[0] == 12345u) *dst = v;   // development diagnostic TQ_S2D_DIAG=2: no stores
+            else *dst = v;
+#endif
           }
     }
   };
@@ -308,12 +326,12 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
           for (int s = 0; s < KS; ++s) {
             const int a = (2 * s + fk) * tout + rt + fr;
             const float mr = mp[0][a], mi = mp[1][a];
-            if (op.pad == 1 || op.pad == 3) {   // development diagnostics: no MFMAs
-              p1[s] = xr[tl][s] * mr;
-              p2[s] = xi[tl][s] * mi;
-              p3[s] = mr + mi;
-              continue;
-            }
+#if TQ_S2D_DIAG == 1 || TQ_S2D_DIAG == 3
+            p1[s] = xr[tl][s] * mr;   // development diagnostics: no MFMAs
+            p2[s] = xi[tl][s] * mi;
+            p3[s] = mr + mi;
+            continue;
+#endif
             p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[tl][s], mr, p1, 0, 0, 0);
             p2 = __builtin_amdgcn_mfma_f32_32x32x2f32(xi[tl][s], mi, p2, 0, 0, 0);
             p3 = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[tl][s] + xi[tl][s], mr + mi, p3, 0, 0, 0);
@@ -344,7 +362,9 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
       f32x16 p1 = {}, p2 = {}, p3 = {};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        if (op.pad == 1) break;   // development diagnostic (TQ_S2D_DIAG=1): no MFMAs
+#if TQ_S2D_DIAG == 1 || TQ_S2D_DIAG == 3
+        break;   // development diagnostics: no MFMAs
+#endif
         const int a = (2 * s + fk) * tout + rt + fr;
         const float mr = mp[0][a], mi = mp[1][a];
         p1 = __builtin_amdgcn_mfma_f32_32x32x2f32(mr, xr[s], p1, 0, 0, 0);
@@ -458,24 +478,20 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
     return std::max(1, cus * std::max(1, per));
   });
   S2DLaunch R = L;
-  static const int diag = [] {
-    const char* e = getenv("TQ_S2D_DIAG");
-    return e ? atoi(e) : 0;
-  }();
-
-  // the round of resident workgroups shared by the ops in proportion to their work: every op
-  // stores the same bytes per output element, and its MFMA work grows with tin (C4's tin-16
-  // left op has twice the products of the tin-8 right op per element)
+  // the round of resident workgroups shared by the ops in proportion to their output: the ops are
+  // bound by their store streams, not their products (C4's tin-16 and tin-8 ops store the same
+  // bytes; shared by products (8 + tin), the tin-8 ops' workgroups finished last: 1.67 vs 1.48 ms
+  // per launch on one box), plus 16 rows' worth per column for the per-column-group work (input
+  // loads, bases: 1.45 ms; 48: 1.48, -16: 1.51)
+  auto work = [&](const S2DOp& o) { return (double)std::max<int64_t>(o.ncols, 1) * (o.tout + 16.0); };
   double wsum = 0;
-  for (int q = 0; q < R.nops; ++q)
-    wsum += (double)std::max<int64_t>(R.op[q].ncols, 1) * R.op[q].tout * (8.0 + R.op[q].tin);
+  for (int q = 0; q < R.nops; ++q) wsum += work(R.op[q]);
   int blocks = 0;
   for (int q = 0; q < R.nops; ++q) {
-    const double wq = (double)std::max<int64_t>(R.op[q].ncols, 1) * R.op[q].tout * (8.0 + R.op[q].tin);
+    const double wq = work(R.op[q]);
     const int want = std::max(1, (int)((double)slots * wq / wsum));
     R.op[q].nblocks = std::max(1, std::min(R.op[q].nblocks, want));
     R.op[q].block_begin = blocks;
-    R.op[q].pad = diag;
     R.op[q].order = order;
     blocks += R.op[q].nblocks;
   }
