@@ -224,6 +224,14 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
                            "achieved_definition": "algorithmic bytes of the step's plans (tq_plan bytes_moved) x "
                                                   "candidate-steps/s",
                            "traffic": None}
+        pm = _profile_json("pmc_c5_r05.json", "C5")
+        if pm and pm.get("hbm_bytes_per_candidate_step"):
+            # HBM bytes per candidate-step (2*FETCH_SIZE + WRITE_SIZE over every kernel of a
+            # c5_bench run / its SGDG dispatches; rocprofv3 PMC passes, scripts/pmc_traffic.sh)
+            out["roofline"]["traffic"] = pm["hbm_bytes_per_candidate_step"]
+            out["roofline"]["traffic_unit"] = "bytes per candidate-step"
+            out["roofline"]["traffic_vs_algorithmic"] = pm["hbm_bytes_per_candidate_step"] / ab
+            out["roofline"]["traffic_source"] = "profiles/pmc_c5_r05.json"
     tr = _profile_json("c5_trace_r04.json", "C5")
     if tr:
         out["gpu_busy_frac"] = tr.get("gpu_busy_frac")
@@ -550,7 +558,11 @@ def main():
             "ms_per_step": sweep_["ms"],
             "algorithmic_bytes_per_step": sweep_["bytes"],
         }
-        pmc_s = _profile_json(f"pmc_{args.config.lower()}_r04.json", args.config)
+        src = f"pmc_{args.config.lower()}_r05.json"
+        pmc_s = _profile_json(src, args.config)
+        if not pmc_s:
+            src = f"pmc_{args.config.lower()}_r04.json"
+            pmc_s = _profile_json(src, args.config)
         if pmc_s and pmc_s.get("sweep_dispatches"):
             # HBM bytes of the sweep launches (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC passes of
             # this command), per launch x this step's launches
@@ -558,7 +570,7 @@ def main():
             res["roofline"]["traffic"] = per * sweep_["launches"]
             res["roofline"]["traffic_unit"] = "bytes per step (sweep launches)"
             res["roofline"]["traffic_vs_algorithmic"] = per * sweep_["launches"] / max(1.0, sweep_["bytes"])
-            res["roofline"]["traffic_source"] = f"profiles/pmc_{args.config.lower()}_r04.json"
+            res["roofline"]["traffic_source"] = f"profiles/{src}"
     if rank == 0:
         _log("permute probe")
         try:

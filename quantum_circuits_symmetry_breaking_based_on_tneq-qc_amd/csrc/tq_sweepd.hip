@@ -483,7 +483,15 @@ int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream) {
   // bytes; shared by products (8 + tin), the tin-8 ops' workgroups finished last: 1.67 vs 1.48 ms
   // per launch on one box), plus 16 rows' worth per column for the per-column-group work (input
   // loads, bases: 1.45 ms; 48: 1.48, -16: 1.51)
-  auto work = [&](const S2DOp& o) { return (double)std::max<int64_t>(o.ncols, 1) * (o.tout + 16.0); };
+  // (TQ_S2D_SHARE=0: by products, the r04 rule, for A/B)
+  static const bool by_products = [] {
+    const char* e = getenv("TQ_S2D_SHARE");
+    return e && e[0] == '0';
+  }();
+  auto work = [&](const S2DOp& o) {
+    const double c = (double)std::max<int64_t>(o.ncols, 1);
+    return by_products ? c * o.tout * (8.0 + o.tin) : c * (o.tout + 16.0);
+  };
   double wsum = 0;
   for (int q = 0; q < R.nops; ++q) wsum += work(R.op[q]);
   int blocks = 0;
