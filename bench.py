@@ -242,18 +242,18 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
     return out
 
 
-def alt_gemm(args, var: str, desc: str):
-    """The same headline with another complex64 boundary-GEMM kernel (env `var`=0, read by the
-    library once per process: a child process, started without exec)."""
+def alt_gemm(args, envs: dict, desc: str):
+    """The same headline with another complex64 boundary-GEMM kernel (library switches in `envs`,
+    read once per process: a child process, started without exec)."""
     import subprocess
-    env = dict(os.environ, **{var: "0"})
+    env = dict(os.environ, **envs)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", args.config, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
     return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
-            "gemm": f"{desc} ({var}=0)", "roofline": d["roofline"]}
+            "gemm": f"{desc} ({' '.join(f'{k}={v}' for k, v in envs.items())})", "roofline": d["roofline"]}
 
 
 def other_config(args, cfg: str):
@@ -584,11 +584,17 @@ def main():
         except Exception as e:  # the baseline must never hide the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
     if world == 1 and rank == 0 and f16 and not args.no_alt:
-        for key, var, desc in (("alt_bf16_split", "TQ_GEMM_F16", "bf16 3-term split, v_mfma_f32_32x32x16_bf16"),
-                               ("alt_f32_mfma", "TQ_GEMM_BF16", "v_mfma_f32_32x32x2_f32")):
+        # the other boundary-GEMM kernels on the same operands (no producer-written planes: the
+        # GEMM splits its operands itself)
+        for key, envs, desc in (
+                ("alt_f16_gemm_side_split", {"TQ_GEMM_PLANES": "0"},
+                 "f16 split inside the GEMM, Gauss 3M on v_mfma_f32_32x32x16_f16 (the r04 default)"),
+                ("alt_bf16_split", {"TQ_GEMM_PLANES": "0", "TQ_GEMM_F16": "0"},
+                 "bf16 3-term split, v_mfma_f32_32x32x16_bf16"),
+                ("alt_f32_mfma", {"TQ_GEMM_PLANES": "0", "TQ_GEMM_BF16": "0"}, "v_mfma_f32_32x32x2_f32")):
             _log(f"alternate GEMM headline: {desc}")
             try:
-                res[key] = alt_gemm(args, var, desc)
+                res[key] = alt_gemm(args, envs, desc)
             except Exception as e:  # the alternate lines must never hide the headline
                 res[key] = {"error": repr(e)}
     if world == 1 and rank == 0 and args.config == "C4" and not args.no_other:
