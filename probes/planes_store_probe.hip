@@ -99,6 +99,89 @@ __global__ void __launch_bounds__(256) store_kernel(_Float16* base, int nblocks_
   }
 }
 
+// var 7: the C4 launch's two op shapes -- regions 0-3 as above (tout 256, 4096 groups), regions
+// 4-7 tout 128 over 8192 groups (same bytes), workgroups split bpr_a / bpr_b; loads as var 5
+// GB: groups per iteration of the tout-128 regions (their loads issued together); GB = 0: no
+// loads, but a vmcnt(0) wait at every group start (the drain of the wave's stores alone)
+template <int GB>
+__global__ void __launch_bounds__(256) store2_kernel(_Float16* base, int bpr_a, int bpr_b, u32x4 v,
+                                                      const uint2* __restrict__ xin) {
+  const bool isb = (int)blockIdx.x >= 4 * bpr_a;
+  const int bpr = isb ? bpr_b : bpr_a;
+  const int rel = isb ? blockIdx.x - 4 * bpr_a : blockIdx.x;
+  const int region = (isb ? 4 : 0) + rel / bpr, blk = rel % bpr;
+  const int tout = isb ? 128 : 256, ngroups = isb ? 8192 : 4096;
+  _Float16* P = base + (long)region * 6 * kPlaneElems;
+  const int lane = threadIdx.x & 63, fr = lane & 31, fk = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = bpr * kWaves;
+  const int nld = isb ? 8 : 16;
+  const int gpi = isb && GB > 0 ? GB : 1;   // groups per iteration
+  for (int g0 = (blk * kWaves + wave) * gpi; g0 < ngroups; g0 += nw * gpi) {
+    unsigned xacc = 0;
+    if constexpr (GB == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+    for (int q = 0; q < gpi; ++q)
+      for (int s2 = 0; s2 < nld && xin; ++s2) xacc ^= xin[((long)region * 8192 + g0 + q) * 512 + s2 * 32 + fr].x;
+    for (int q = 0; q < gpi; ++q)
+    for (int rt = 0; rt < tout; rt += 32) {
+      const long gb = (long)(g0 + q) * 64 * tout;
+      const long rb = gb + 64L * (rt + fr) + 8 * fk;
+      u32x4 w = v;
+      w.x ^= xacc;
+#pragma unroll
+      for (int pl = 0; pl < 6; ++pl)
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            u32x4* dst = reinterpret_cast<u32x4*>(P + pl * kPlaneElems + rb + 32 * tl + 16 * h);
+            *dst = w;
+          }
+    }
+  }
+}
+
+// var 8: the two-shape launch with the input reads issued as LDS-DMA (global_load_lds_dwordx4 into
+// a per-wave LDS scratch) and never waited for: the reads' DRAM traffic without any wave waiting
+// on them
+__global__ void __launch_bounds__(256) store3_kernel(_Float16* base, int bpr_a, int bpr_b, u32x4 v,
+                                                      const uint2* __restrict__ xin) {
+  __shared__ __attribute__((aligned(16))) unsigned char scratch[kWaves][1024];
+  const bool isb = (int)blockIdx.x >= 4 * bpr_a;
+  const int bpr = isb ? bpr_b : bpr_a;
+  const int rel = isb ? blockIdx.x - 4 * bpr_a : blockIdx.x;
+  const int region = (isb ? 4 : 0) + rel / bpr, blk = rel % bpr;
+  const int tout = isb ? 128 : 256, ngroups = isb ? 8192 : 4096;
+  _Float16* P = base + (long)region * 6 * kPlaneElems;
+  const int lane = threadIdx.x & 63, fr = lane & 31, fk = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = bpr * kWaves;
+  const int ndma = isb ? 4 : 8;   // x 1 KiB = the group's 16 x 256 B (A) / 8 x 256 B (B) of reads... x2
+  const unsigned lds = (unsigned)(uintptr_t)&scratch[wave][0];
+  for (int g = blk * kWaves + wave; g < ngroups; g += nw) {
+    const char* src = reinterpret_cast<const char*>(xin + ((long)region * 8192 + g) * 512);
+    for (int d = 0; d < ndma; ++d) {
+      const char* a = src + d * 1024 + lane * 16;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" :: "s"(lds), "v"(a) : "memory", "m0");
+    }
+    const long gb = (long)g * 64 * tout;
+    for (int rt = 0; rt < tout; rt += 32) {
+      const long rb = gb + 64L * (rt + fr) + 8 * fk;
+#pragma unroll
+      for (int pl = 0; pl < 6; ++pl)
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            u32x4* dst = reinterpret_cast<u32x4*>(P + pl * kPlaneElems + rb + 32 * tl + 16 * h);
+            *dst = v;
+          }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // linear fill of the same bytes (the ceiling: every wave writes consecutive 1-KiB blocks)
 __global__ void __launch_bounds__(256) fill_kernel(u32x4* base, long n16, u32x4 v) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256) base[i] = v;
@@ -125,7 +208,7 @@ int main(int argc, char** argv) {
   _Float16* buf = nullptr;
   if (hipMalloc(&buf, bytes) != hipSuccess) return 1;
   const u32x4 v = {0x3c003c00u, 0x3c003c00u, 0x3c003c00u, 0x3c003c00u};
-  uint2* xin = nullptr;   // inputs: 8 regions x 4096 groups x 1024 x 8 B (256 MiB)
+  uint2* xin = nullptr;   // inputs: 8 regions x 4096 groups x 1024 x 8 B (256 MiB; var 7: 8192 x 512)
   if (hipMalloc(&xin, (size_t)kRegions * kGroups * 1024 * 8) != hipSuccess) return 1;
   (void)hipMemset(xin, 0, (size_t)kRegions * kGroups * 1024 * 8);
   const double gb = bytes / 1e9;
@@ -140,6 +223,17 @@ int main(int argc, char** argv) {
   report("contig1K_nt", time_ms([&] { hipLaunchKernelGGL(store_kernel<3>, grid, dim3(256), 0, 0, buf, bpr, v, xin); }, 5));
   report("rows32B_xload", time_ms([&] { hipLaunchKernelGGL(store_kernel<5>, grid, dim3(256), 0, 0, buf, bpr, v, xin); }, 5));
   report("rows32B_xprefetch", time_ms([&] { hipLaunchKernelGGL(store_kernel<6>, grid, dim3(256), 0, 0, buf, bpr, v, xin); }, 5));
+  for (int ba : {48, 64, 80}) {
+    const int bb = 128 - ba;
+    char name[64];
+    snprintf(name, sizeof name, "twoshapes_xload_a%d_b%d", ba, bb);
+    report(name, time_ms([&] { hipLaunchKernelGGL(store2_kernel<1>, dim3(4 * ba + 4 * bb), dim3(256), 0, 0, buf, ba, bb, v, xin); }, 5));
+  }
+  report("twoshapes_xload_b2groups", time_ms([&] { hipLaunchKernelGGL(store2_kernel<2>, dim3(4 * 64 + 4 * 64), dim3(256), 0, 0, buf, 64, 64, v, xin); }, 5));
+  report("twoshapes_xload_b4groups", time_ms([&] { hipLaunchKernelGGL(store2_kernel<4>, dim3(4 * 64 + 4 * 64), dim3(256), 0, 0, buf, 64, 64, v, xin); }, 5));
+  report("twoshapes_drain_only", time_ms([&] { hipLaunchKernelGGL(store2_kernel<0>, dim3(4 * 64 + 4 * 64), dim3(256), 0, 0, buf, 64, 64, v, xin); }, 5));
+  report("twoshapes_dma_nowait", time_ms([&] { hipLaunchKernelGGL(store3_kernel, dim3(4 * 64 + 4 * 64), dim3(256), 0, 0, buf, 64, 64, v, xin); }, 5));
+  report("twoshapes_noload", time_ms([&] { hipLaunchKernelGGL(store2_kernel<1>, dim3(4 * 64 + 4 * 64), dim3(256), 0, 0, buf, 64, 64, v, (const uint2*)nullptr); }, 5));
   report("contig1K_plinner", time_ms([&] { hipLaunchKernelGGL(store_kernel<4>, grid, dim3(256), 0, 0, buf, bpr, v, xin); }, 5));
   hipFree(buf);
   return 0;

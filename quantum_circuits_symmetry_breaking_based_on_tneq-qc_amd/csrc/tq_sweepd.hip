@@ -93,6 +93,8 @@ struct SdSmem {
   int32_t ooff[kS2DMaxTout];
   int64_t btab[2][kLevels][64];
   int64_t wcol[2][kS2MaxColBits];
+  // planes mode: each wave's next 64-column group of X, [k][64 columns] (LDS-DMA target)
+  __attribute__((aligned(16))) float2 xs[kWaves][TMAX * 64];
 };
 
 // one op's share of the launch (its workgroups stride over its 32-column tiles)
@@ -305,18 +307,63 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
     // 64-column groups (column bits 0..5), the same products with the operands swapped (the
     // transposed tile: columns in registers)
     const int64_t ngroups = ntiles >> 1;
-    for (int64_t g = (int64_t)blk * kWaves + wave; g < ngroups; g += nw) {
+    int64_t g_0 = (int64_t)blk * kWaves + wave, g_end = ngroups, g_step = nw;
+    if (op.order == 1) {   // blocked: each wave its own contiguous range of groups
+      const int64_t per = (ngroups + nw - 1) / nw;
+      g_0 = ((int64_t)blk * kWaves + wave) * per;
+      g_end = ngroups < g_0 + per ? ngroups : g_0 + per;
+      g_step = 1;
+    }
+    // The group's inputs arrive by LDS-DMA into the wave's slot, issued at the previous group's
+    // start (right after that group's inputs left the slot): the group waits with vmcnt(N), N the
+    // stores issued after the DMA (up to 63), not vmcnt(0) -- a register load at the group start
+    // waited for every store the wave had in flight and then for the load itself behind the
+    // saturated write stream (probes/planes_store_probe.hip: 1.69 -> 1.45 ms for the launch's
+    // store pattern with its reads, issued without waits)
+    const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&sm.xs[wave][0]);
+    const char* const Xb = reinterpret_cast<const char*>(op.X);
+    // SGPR base (the group's column base, uniform) + a 32-bit lane byte offset per instruction
+    // (loop invariant): no 64-bit address VGPRs in the group loop
+    uint32_t doff[KS];
+#pragma unroll
+    for (int i = 0; i < KS; ++i) doff[i] = (uint32_t)((io[i] + 2 * fr) * 8);
+    auto dma = [&](int64_t g) {   // X[k][64 columns of group g] -> slot, KS x 1 KiB
       const int64_t bi = base(0, g);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bi), hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)bi >> 32));
+      const char* const gbase = Xb + (int64_t)(((uint64_t)hi << 32) | lo) * 8;
+#pragma unroll
+      for (int i = 0; i < KS; ++i) {
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(doff[i]), "s"(gbase), "s"(slot + 1024u * i) : "memory");
+      }
+    };
+    const int nrt = tout / 32;
+    if (g_0 < g_end) {
+      dma(g_0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    for (int64_t g = g_0; g < g_end; g += g_step) {
       float xr[2][KS], xi[2][KS];
+      {
+        const float2* xsl = sm.xs[wave];
 #pragma unroll
-      for (int tl = 0; tl < 2; ++tl)
+        for (int tl = 0; tl < 2; ++tl)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const f2v v = X[bi + io[s] + 32 * tl + fr];
-          xr[tl][s] = ldexpf(v.x, xsc);
-          xi[tl][s] = ldexpf(v.y, xsc);
-        }
+          for (int s = 0; s < KS; ++s) {
+            const float2 v = xsl[(2 * s + fk) * 64 + 32 * tl + fr];
+            xr[tl][s] = ldexpf(v.x, xsc);
+            xi[tl][s] = ldexpf(v.y, xsc);
+          }
+      }
+      // every lane's reads of the slot are complete before the next DMA overwrites it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // (unconditional: the last group re-reads its own inputs -- a branch here doubled the
+      // kernel's registers)
+      const bool more = g + g_step < g_end;
+      dma(more ? g + g_step : g);
       const int64_t gb = base(1, g);
+#pragma unroll 1
       for (int rt = 0; rt < tout; rt += 32) {
         f32x16 d[2][2];
 #pragma unroll
@@ -341,6 +388,11 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
         }
         emit_planes(d, gb, rt);
       }
+      // the next group's DMA is older than this group's 24 x nrt stores: all but the most recent
+      // min(63, 24 nrt) operations complete => the DMA has landed
+      if (nrt >= 3) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+      else if (nrt == 2) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
     }
     return;
   }
@@ -384,7 +436,10 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
 // TB == 0: every op of the launch has input tile TA; else each op has TA or TB (one dependency
 // level's dense ops of both subtrees of a cut network in one launch: their tails overlap)
 template <int TA, int TB, bool NTS>
-__global__ void __launch_bounds__(64 * kWaves) sweepd_kernel(S2DLaunch L) {
+#ifndef TQ_S2D_OCC
+#define TQ_S2D_OCC 2
+#endif
+__global__ void __launch_bounds__(64 * kWaves, TQ_S2D_OCC) sweepd_kernel(S2DLaunch L) {
   constexpr int TMAX = TA > TB ? TA : TB;
   __shared__ SdSmem<TMAX> sm;
   int j = 0;
