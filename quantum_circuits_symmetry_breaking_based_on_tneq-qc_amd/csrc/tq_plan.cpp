@@ -1246,6 +1246,14 @@ class Compiler {
     }();
     return v;
   }
+  // TQ_S2_WAVELOCAL=0: a workgroup barrier between every two sweep2 passes
+  static bool s2_wave_local() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_WAVELOCAL");
+      return !(e && atoi(e) == 0);
+    }();
+    return v;
+  }
   static int s2_min_logc() {
     static const int v = [] {
       const char* e = getenv("TQ_S2_MINLC");
@@ -1892,6 +1900,31 @@ class Compiler {
         const int g = d.k.pmeta[q][kS2PmFirst];
         if (g != q) std::copy(d.k.lut[g], d.k.lut[g] + 64, d.k.lut[q]);
       }
+      // Barriers between passes (kS2PmSync, bit 16 of a pass's count word: the workgroup barrier
+      // before that pass).  Thread t of the 512 takes the groups gi = t (mod 512) in every pass
+      // (tq_sweep2.hip gate_pass_u / block_pass), so wave w owns the groups whose gi bits 6..8 are
+      // w, i.e. the elements whose address bits behind those group bits (columns below logC, then
+      // the pass positions in ascending order) are w.  Two consecutive passes with the same
+      // wave-select address bits leave every element with one wave: no barrier between them (LDS
+      // accesses of one wave complete in order).
+      auto wave_sig = [&](int q) {
+        const uint32_t mask = (uint32_t)d.k.pmeta[q][kS2PmPass];
+        const int lg = d.logC + __builtin_popcount(mask);   // log2 groups
+        std::vector<int> sig;
+        for (int b = 6; b <= 8 && b < lg; ++b) {
+          if (b < d.logC) { sig.push_back(-1 - b); continue; }
+          uint32_t m = mask;
+          for (int t = 0; t < b - d.logC; ++t) m &= m - 1;
+          sig.push_back(__builtin_ctz(m));
+        }
+        return sig;
+      };
+      d.nsync = 0;
+      for (int q = 0; q < d.npass; ++q) {
+        const bool sync = q == 0 || !s2_wave_local() || wave_sig(q) != wave_sig(q - 1);
+        if (sync) d.k.pmeta[q][kS2PmCount] |= kS2PmSync;
+        d.nsync += sync;
+      }
     }
     if (getenv("TQ_DEBUG_S2")) {
       fprintf(stderr, "S2 cols=2^%d logC=%d used=%d epi=%d ld:", d.colbits, d.logC, used, d.epi);
@@ -1976,7 +2009,7 @@ class Compiler {
     if (d.epi) o << " epi";
     {
       char b[48];
-      snprintf(b, sizeof b, " ldsx=%.2f->%.2f", d.lds_model[0], d.lds_model[1]);
+      snprintf(b, sizeof b, " ldsx=%.2f->%.2f syncs=%d/%d", d.lds_model[0], d.lds_model[1], d.nsync, d.npass);
       o << b;
     }
     op.note = o.str();

@@ -99,6 +99,7 @@ struct S2Desc {
   // modeled extra LDS bank-conflict cycles / conflict-free cycles of a chunk: the r04 column-only
   // swizzle, the chosen one (tq_plan.cpp s2_layout)
   float lds_model[2] = {};
+  int32_t nsync = 0;             // passes preceded by a workgroup barrier (kS2PmSync)
   alignas(8) S2Gate gate[kS2MaxGates];
 };
 constexpr int kS2KeepOff = (int)offsetof(S2Desc, k);
@@ -107,6 +108,7 @@ static_assert(kS2KeepOff % 8 == 0 && kS2DescHotBytes % 8 == 0, "descriptor copy 
 constexpr int kS2GmK = 0, kS2GmN = 1, kS2GmPass = 2, kS2GmKaddr = 3, kS2GmNaddr = kS2GmKaddr + kS2MaxK;
 static_assert(kS2GmNaddr + kS2MaxKN <= 16, "gate meta layout");
 constexpr int kS2PmFirst = 0, kS2PmCount = 1, kS2PmB = 2, kS2PmPass = 3, kS2PmAddr = 4, kS2PmCode = 8;
+constexpr int kS2PmSync = 1 << 16;   // count-word flag: a workgroup barrier before this pass
 constexpr int kS2BlkMaxGates = 8;      // gates per register block
 inline int s2_block_bits(int esz, int64_t tile_elems) {
   // 2^B elements per thread: 16 (FP32 data, tiles of >= 8192 elements) or 8

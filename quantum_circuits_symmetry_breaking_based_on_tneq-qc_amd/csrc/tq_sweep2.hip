@@ -415,7 +415,7 @@ __device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restr
       if ((e >> b) & 1) o ^= ba[b];
     return o;
   };
-  const int first = pm[kS2PmFirst], cnt = pm[kS2PmCount];
+  const int first = pm[kS2PmFirst], cnt = pm[kS2PmCount] & 0xff;
   for (int g0 = threadIdx.x; g0 < ngroups; g0 += NT) {
     const int gp = g0 >> logC;
     int a0 = lut[gp & 31] ^ lut[32 + (gp >> 5)] ^ ((g0 << SH) & cmb);
@@ -434,7 +434,7 @@ template <typename T>
 __device__ __forceinline__ void run_gate(T* buf, const T* cf, const PassHead& h, const int32_t* lut, int logC) {
 #define TQ_GATE(k, n) \
   case k * 16 + n: gate_pass<T, k, n>(buf, cf, h, lut, logC); break;
-  switch (h.w[kS2PmCount] >> 8) {   // K * 16 + N
+  switch ((h.w[kS2PmCount] >> 8) & 0xff) {   // K * 16 + N
     TQ_GATE(1, 1) TQ_GATE(1, 2) TQ_GATE(1, 4) TQ_GATE(1, 8)
     TQ_GATE(2, 1) TQ_GATE(2, 2) TQ_GATE(2, 4) TQ_GATE(2, 8)
     TQ_GATE(4, 1) TQ_GATE(4, 2) TQ_GATE(4, 4) TQ_GATE(4, 8)
@@ -781,6 +781,11 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     for (int p = 0; p < npass; ++p) {
       PassHead cur;
       read_head(p, cur);
+      // the workgroup barrier before a pass only where another wave may own its elements
+      // (kS2PmSync, tq_plan.cpp s2_layout); otherwise every element this pass touches was
+      // last touched by this wave, whose LDS accesses complete in order
+      if (p > 0 && (cur.w[kS2PmCount] & kS2PmSync)) __syncthreads();
+      asm volatile("" ::: "memory");
       const int g = cur.w[kS2PmFirst];
       const int bk = cur.w[kS2PmB];
       const int32_t* const lp = lut + p * kLut;   // the pass's group table (rows by pass)
@@ -789,7 +794,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
         if constexpr (sizeof(T) <= 8) block_pass<T, 4>(buf, cf, cur, pmeta + p * 16, lp, logC);
       }
       else block_pass<T, 3>(buf, cf, cur, pmeta + p * 16, lp, logC);
-      __syncthreads();
+      asm volatile("" ::: "memory");
 #ifdef TQ_S2_TIMING
       if (ch == lb && ts_rec && threadIdx.x == 0 && p < 16) {
         g_s2_ts[ts_idx][9 + p] = clock64() - clk0;
@@ -798,6 +803,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
       }
 #endif
     }
+    __syncthreads();   // the store phase reads the tile in its own enumeration
     if (ch == lb) TQ_TS(4);
 #ifdef TQ_S2_TIMING
     if (ch == lb) clk_gates = clock64() - clk0;
