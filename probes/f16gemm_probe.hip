@@ -788,9 +788,132 @@ __global__ void __launch_bounds__(NT) gemm6(Args g) {
       }
 }
 
+// VAR & 512 (gemm7): one wave per SIMD -- 4 waves (2 x 2) of 128 x 128 on the same 256 x 256
+// workgroup tile and LDS image as gemm3 (accumulators 256 registers, fragments 128): half the
+// fragment reads per MFMA, no partner wave on the SIMD (latency hidden inside the wave: every
+// fragment read of a step issued ahead of the MFMAs that need it).  VAR & 1024: the step's
+// reads in three groups, each issued under the previous term's MFMAs.
+constexpr int NT7 = 256;
+template <int VAR>
+__global__ void __launch_bounds__(NT7, 1) gemm7(Args g) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 4 * TB3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int nt = g.N / BN, ntile = (g.M / BM) * nt;
+  const int tile = L % ntile, grp = L / ntile;
+  const int split = grp % g.splits, b = grp / g.splits;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
+  const long long K1 = g.K / 3;
+  const long long k0 = split * (K1 / g.splits);
+  const int nk = (int)(K1 / g.splits / BK3);
+  const int lane_i = b / 3, prod = b % 3;
+  const long long psA = K1 * g.M, psB = K1 * g.N;
+  const _Float16* Ah = g.A + (long long)lane_i * 6 * psA + (2 * prod) * psA + k0 * g.M + m0;
+  const _Float16* Bh = g.B + (long long)lane_i * 6 * psB + (2 * prod) * psB + k0 * g.N + n0;
+  uint32_t goA[4], goB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 2 * (4 * i + w) + (lane >> 5);
+    const int c = ((lane & 31) >> 1) ^ fsw(r);
+    goA[i] = (uint32_t)(r * g.M + c * 16 + (lane & 1) * 8) * 2;
+    goB[i] = (uint32_t)(r * g.N + c * 16 + (lane & 1) * 8) * 2;
+  }
+  const unsigned lbase = (unsigned)(uintptr_t)(LDS char*)lds;
+  auto glds16 = [&](const _Float16* base, uint32_t voff, unsigned off) {
+    unsigned keep;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lbase + off);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(base), "s"(dst) : "memory");
+  };
+  auto stage = [&](int t, int buf) {
+    const _Float16* pa = Ah + (long long)t * BK3 * g.M;
+    const _Float16* pb = Bh + (long long)t * BK3 * g.N;
+    const unsigned o = buf * 4 * TB3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(pa, goA[i], o + (4 * i + w) * 1024);
+      glds16(pa + psA, goA[i], o + TB3 + (4 * i + w) * 1024);
+      glds16(pb, goB[i], o + 2 * TB3 + (4 * i + w) * 1024);
+      glds16(pb + psB, goB[i], o + 3 * TB3 + (4 * i + w) * 1024);
+    }
+  };
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int x = q | ((g4 & 1) << 2);
+  const int rowb = (8 * g4 + q) * (BM * 2) + 8 * p;
+  int aoff[8], boff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) aoff[i] = rowb + ((wm * 8 + i) ^ x) * 32;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) boff[j] = 2 * TB3 + rowb + ((wn * 8 + j) ^ x) * 32;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto rd = [&](const char* s, int off) -> f16x8 {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS s16x4*)(s + off + 4 * BM * 2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const char* s = lds + (t & 1) * 4 * TB3;
+    if (t + 1 < nk) stage(t + 1, (t & 1) ^ 1);
+    f16x8 ah[8], al[8], bh[8], bl[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bh[j] = rd(s, boff[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ah[i] = rd(s, aoff[i]);
+    if constexpr (!(VAR & 1024)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bl[j] = rd(s, boff[j] + TB3);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) al[i] = rd(s, aoff[i] + TB3);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    if constexpr (VAR & 1024) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bl[j] = rd(s, boff[j] + TB3);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) al[i] = rd(s, aoff[i] + TB3);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  float* C = g.C + ((long long)(b * g.splits + split) * g.M) * g.N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + i * 16 + g4 * 4 + r;
+        const int n = n0 + wn * 128 + j * 16 + (lane & 15);
+        C[(long long)m * g.N + n] = acc[i][j][r];
+      }
+}
+
 template <int VAR>
 static void launch(int nwg, const Args& g) {
-  if constexpr (VAR & 256) hipLaunchKernelGGL(gemm6<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
+  if constexpr (VAR & 512) hipLaunchKernelGGL(gemm7<VAR>, dim3(nwg), dim3(NT7), 0, 0, g);
+  else if constexpr (VAR & 256) hipLaunchKernelGGL(gemm6<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
   else if constexpr (VAR & 64) hipLaunchKernelGGL(gemm5<VAR>, dim3(nwg * 2), dim3(NT), 0, 0, g);
   else if constexpr (VAR & 32) hipLaunchKernelGGL(gemm4<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
   else if constexpr (VAR & 4) hipLaunchKernelGGL(gemm3<VAR>, dim3(nwg), dim3(NT), 0, 0, g);
@@ -922,6 +1045,8 @@ int main(int argc, char** argv) {
   if (v == 0 || v == 10) run<52>("pipelined_terms_stamps", g, nwg, false);
   if (v == 0 || v == 13) run<148>("fused_terms_waitstamps", g, nwg, false);
   if (v == 0 || v == 14) run<260>("pingpong", g, nwg, true);
+  if (v == 0 || v == 17) run<516>("onewave_128x128", g, nwg, true);
+  if (v == 0 || v == 18) run<1540>("onewave_128x128_readsplit", g, nwg, true);
   if (v == 0 || v == 15) run<276>("pingpong_stamps", g, nwg, false);
   if (v == 0 || v == 16) run<261>("pingpong_setprio", g, nwg, false);
   if (v == 0 || v == 11) run<68>("tile256x128_3stage", g, nwg, true);
