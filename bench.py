@@ -88,23 +88,36 @@ def _cpu_model() -> str:
 
 
 def _cpu_sample(t, n_sl, min_seconds, threads):
-    """Whole slices of the oracle's complex64 executor at `threads` BLAS threads until
-    ~min_seconds of CPU work: (slices timed, seconds, BLAS threads in effect).  A network with
-    fewer slices than that takes (C2: one, unsliced) is contracted again, slice by slice."""
+    """The oracle's complex64 executor on the sliced job at `threads` BLAS threads, hoisting the
+    slice-invariant steps once as the GPU plan does (oracle.contract_ref.contract_sliced): the
+    whole job timed when it fits ~min_seconds (repeated up to that budget), else one slice and two
+    slices timed and the per-slice part extrapolated to all slices.  Returns (seconds per whole job,
+    sample description, BLAS threads in effect)."""
     import numpy as np
-    from oracle.contract_ref import contract as ref_contract, sliced_operands
+    from oracle.contract_ref import contract_sliced
     from threadpoolctl import threadpool_info, threadpool_limits
     ops64 = [o.astype(np.complex64) for o in t.operands]
+    sliced = list(t.sliced)
+
+    def run(ids):
+        t0 = time.perf_counter()
+        contract_sliced(t.eq, ops64, sliced, t.path, slice_ids=ids, exact=False)
+        return time.perf_counter() - t0
+
     with threadpool_limits(limits=threads):
         used = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
-        done, dt = 0, 0.0
-        while dt < min_seconds and (done < n_sl or dt < 0.5 * min_seconds):
-            eq, sops = sliced_operands(t.eq, ops64, t.sliced, done % n_sl)
-            t0 = time.perf_counter()
-            ref_contract(eq, *sops, path=t.path, exact=False)
-            dt += time.perf_counter() - t0
-            done += 1
-    return done, dt, used
+        t1 = run([0])
+        t2 = run([0, 1]) if n_sl > 1 else t1
+        per = max(t2 - t1, 0.0) if n_sl > 1 else t1
+        once = max(t1 - per, 0.0)
+        if once + n_sl * per <= min_seconds:
+            done, dt = 0, 0.0
+            while done == 0 or dt < 0.5 * min_seconds:
+                dt += run(list(range(n_sl)))
+                done += 1
+            return dt / done, f"the whole job ({n_sl} slices, hoisted steps once) timed {done}x ({dt:.2f} s)", used
+        return once + n_sl * per, (f"1 and 2 slices timed ({t1:.2f} / {t2:.2f} s): hoisted part {once:.2f} s "
+                                   f"+ {n_sl} x {per:.2f} s per slice"), used
 
 
 def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
@@ -130,9 +143,8 @@ def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
     runs = []
     for th in sorted({host, min(16, host)}, reverse=True):
         _log(f"cpu baseline at {th} BLAS threads")
-        done, dt, used = _cpu_sample(t, n_sl, min_seconds if th == host else min_seconds / 2, th)
-        runs.append({"value": n_amp / (n_sl * dt / done), "cores": used,
-                     "sample": f"{done} slice contractions of {n_sl} timed ({dt:.2f} s)"})
+        job_s, sample, used = _cpu_sample(t, n_sl, min_seconds if th == host else min_seconds / 2, th)
+        runs.append({"value": n_amp / job_s, "cores": used, "sample": sample})
     best = max(runs, key=lambda r: r["value"])
     return {
         "value": best["value"],
@@ -145,9 +157,8 @@ def cpu_baseline(circ_cfg: str, min_seconds: float = 12.0):
         "cpu_model": _cpu_model(),
         "by_threads": runs,
         "sample": (f"oracle = numpy pairwise transpose+matmul executor in complex64 (the GPU dtype) on "
-                   f"the {circ_cfg} network, same path/cut/slicing, {n_amp} amplitudes; whole slices timed "
-                   f"(repeated when there are fewer than the time budget needs) and extrapolated linearly to "
-                   f"all {n_sl}, at BLAS threads = every host core "
+                   f"the {circ_cfg} network, same path/cut/slicing, {n_amp} amplitudes, slice-invariant steps "
+                   f"once per job (as the GPU plan hoists them); {n_sl} slices, at BLAS threads = every host core "
                    f"({host}) and = 16; value = the faster ({best['cores']} threads: {best['sample']})"),
     }
 
@@ -242,17 +253,17 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
     return out
 
 
-def alt_gemm(args, envs: dict, desc: str):
-    """The same headline with another complex64 boundary-GEMM kernel (library switches in `envs`,
+def alt_gemm(args, envs: dict, desc: str, cfg: str):
+    """Config `cfg` with another complex64 boundary-GEMM kernel (library switches in `envs`,
     read once per process: a child process, started without exec)."""
     import subprocess
     env = dict(os.environ, **envs)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", args.config, "--steps", str(args.steps),
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
-    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
+    return {"config": cfg, "value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
             "gemm": f"{desc} ({' '.join(f'{k}={v}' for k, v in envs.items())})", "roofline": d["roofline"]}
 
 
@@ -303,7 +314,9 @@ def main():
     ap.add_argument("--save-out", default=None, help="rank 0 saves the last step's amplitudes (.npy)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4"])
+    ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C3d", "C4g"],
+                    help="C4g: C4 on the big-boundary-GEMM path (each half swept whole); "
+                         "C3d: C3 with deferred sweep tails (circuits.config_task)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 training-step line")
     ap.add_argument("--no-alt", action="store_true",
@@ -583,9 +596,9 @@ def main():
             res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         except Exception as e:  # the baseline must never hide the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
-    if world == 1 and rank == 0 and f16 and not args.no_alt:
-        # the other boundary-GEMM kernels on the same operands (no producer-written planes: the
-        # GEMM splits its operands itself)
+    if world == 1 and rank == 0 and f16 and not args.no_alt and args.config in ("C4", "C4g"):
+        # the other boundary-GEMM kernels on the big-GEMM path's operands (C4g; no producer-written
+        # planes: the GEMM splits its operands itself)
         for key, envs, desc in (
                 ("alt_f16_gemm_side_split", {"TQ_GEMM_PLANES": "0"},
                  "f16 split inside the GEMM, Gauss 3M on v_mfma_f32_32x32x16_f16 (the r04 default)"),
@@ -594,11 +607,12 @@ def main():
                 ("alt_f32_mfma", {"TQ_GEMM_PLANES": "0", "TQ_GEMM_BF16": "0"}, "v_mfma_f32_32x32x2_f32")):
             _log(f"alternate GEMM headline: {desc}")
             try:
-                res[key] = alt_gemm(args, envs, desc)
+                res[key] = alt_gemm(args, envs, desc, "C4g")
             except Exception as e:  # the alternate lines must never hide the headline
                 res[key] = {"error": repr(e)}
     if world == 1 and rank == 0 and args.config == "C4" and not args.no_other:
-        for cfg in ("C2", "C3"):
+        # C4g: the same amplitudes on the big-boundary-GEMM path (the planes GEMM's roofline)
+        for cfg in ("C2", "C3", "C4g"):
             _log(f"secondary config {cfg}")
             try:
                 res[f"config_{cfg}"] = other_config(args, cfg)

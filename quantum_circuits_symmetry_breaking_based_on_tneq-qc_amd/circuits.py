@@ -15,13 +15,13 @@ gate or vector: the APPLY lowering), the halves meet in one boundary GEMM over t
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
 from .contractor.einsum_strategy import EinsumStrategy
 from .core.qctn import QCTN
-from .einsum import (Network, choose_slices, get_symbol, linear_path, parse_equation, partition_path,
+from .einsum import (Network, choose_slices, deferred_search, get_symbol, linear_path, parse_equation, partition_path,
                      vector_absorptions)
 
 
@@ -164,10 +164,12 @@ class AmplitudeTask:
 
 def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Optional[Dict[int, int]] = None,
                    cut: Optional[int] = None, n_slice: int = 0, bit_seed: int = 7,
-                   absorb_vectors: bool = True, tile: int = 4) -> AmplitudeTask:
+                   absorb_vectors: bool = True, tile: int = 4,
+                   defer: Union[None, str, Tuple[int, int]] = None) -> AmplitudeTask:
     """Build the amplitude network; fixed bits default to a seeded uniform bitstring.
     With a cut, each half is swept in diamond tiles of `tile` x `tile` gates (diamond_order;
-    0 = line by line)."""
+    0 = line by line); `defer` = (left, right) tensors at the end of each half's sweep absorbed
+    after the boundary contraction (einsum.partition_path), "auto" = einsum.deferred_search."""
     n = circ.n_qubits
     open_set = set(int(q) for q in open_qubits)
     if fixed_bits is None:
@@ -235,6 +237,11 @@ def amplitude_task(circ: BrickWall, open_qubits: Sequence[int], fixed_bits: Opti
         rm = set(m for i in right for m in net.terms[i])
         cut_modes = sorted((lm & rm) - set(net.out))
         sliced_ids = choose_slices(net, path, n_slice, cut_modes) if n_slice else []
+        if defer == "auto":
+            defer = deferred_search(net, [left, right], [lord, rord], pre, sliced_ids)
+        if defer and any(defer):
+            path = partition_path(net, [left, right], [lord, rord], pre=pre, defer=defer)
+            sliced_ids = choose_slices(net, path, n_slice, cut_modes) if n_slice else []
     return AmplitudeTask(circ, eq, shapes, operands, kinds, list(open_q), dict(fixed_bits), path,
                          [net.symbols[m] for m in sliced_ids], cut)
 
@@ -289,7 +296,16 @@ def config_task(name: str, seed: int = 0) -> AmplitudeTask:
         return amplitude_task(BrickWall(30, 14, seed), [])
     if name == "C3":   # 40q d16, cut 20|20, 8+8 open, 6 sliced cut legs -> 64 slices
         return amplitude_task(BrickWall(40, 16, seed), list(range(12, 28)), cut=20, n_slice=6)
+    if name == "C3d":  # C3 with deferred tails (10 / 8): 3.2e9 -> 5.3e8 complex MACs, but measured
+        # slower (1.74 vs 0.68 ms per execute, profiles/defer_sweep_r05.txt): the per-slice tails run
+        # as per-lane launches, where C3's per-slice boundary GEMMs run lane-batched
+        return amplitude_task(BrickWall(40, 16, seed), list(range(12, 28)), cut=20, n_slice=6, defer=(10, 8))
     if name == "C4":   # 53q d20, cut 27|26, 10+10 open, 3 sliced cut legs -> 8 slices
+        # the last 20 / 16 tensors of the two sweeps absorbed after the boundary contraction
+        # (einsum.deferred_search on this network: 5.6e11 -> 3.5e9 complex MACs per execute)
+        return amplitude_task(BrickWall(53, 20, seed), list(range(17, 37)), cut=27, n_slice=3, defer=(20, 16))
+    if name == "C4g":  # C4 on the r02-r05 path: each half swept whole, then ONE boundary contraction
+        # (per slice a 1024 x 1024 x 65536 complex GEMM fed by the dense sweeps: the big-GEMM path)
         return amplitude_task(BrickWall(53, 20, seed), list(range(17, 37)), cut=27, n_slice=3)
     raise ValueError(f"unknown config {name!r}")
 

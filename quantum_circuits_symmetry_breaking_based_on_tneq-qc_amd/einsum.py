@@ -277,17 +277,40 @@ def _linear_on_state(st: _State, ids: Sequence[int], rank: Dict[int, int], stric
 
 def partition_path(net: Network, groups: Sequence[Sequence[int]],
                    orders: Optional[Sequence[Sequence[int]]] = None,
-                   pre: Sequence[Tuple[int, int]] = (), strict: bool = False) -> List[Tuple[int, int]]:
+                   pre: Sequence[Tuple[int, int]] = (), strict: bool = False,
+                   defer: Optional[Sequence[int]] = None) -> List[Tuple[int, int]]:
     """Sweep each group with linear_path, then contract the group results left to right.
     `pre` pairs (original ids, both in one group) are contracted before the sweeps; `strict`
-    follows each order hint exactly (see _linear_on_state)."""
+    follows each order hint exactly (see _linear_on_state).
+
+    `defer[g]` = the number of tensors at the END of group g's sweep that are not absorbed into
+    the group result but into the contracted boundary afterwards (greedily, smallest result first).
+    A sweep's last tensors are the gates that grow it into the boundary operand -- they add the
+    open legs and the cut legs the other side contracts -- so absorbing them after the boundary
+    contraction shrinks that contraction by orders of magnitude (C4: the 2^36-MAC boundary GEMM
+    per slice becomes a 2^31-MAC one over the cut legs those gates do not touch; deferred_search
+    picks the counts by the path cost model)."""
     st = _State(net)
     path, find = _apply_pre(st, pre)
     roots = []
+    later: List[int] = []
     for g, grp in enumerate(groups):
         order = orders[g] if orders is not None else list(grp)
         rank0 = {t: k for k, t in enumerate(order)}
         ids, rank = _alias_group(list(grp), find, rank0)
+        t = int(defer[g]) if defer is not None and g < len(defer) else 0
+        if t > 0:
+            # the sweep's absorption order on a scratch state, then the sweep without its tail
+            seq = _sweep_sequence(st, ids, rank, strict)
+            t = min(t, len(seq) - 1)
+            keep, tail = seq[:len(seq) - t], seq[len(seq) - t:]
+            cur = keep[0]
+            for nxt in keep[1:]:
+                path.append((cur, nxt))
+                cur = st.contract(cur, nxt)
+            roots.append(cur)
+            later += tail
+            continue
         p, root = _linear_on_state(st, ids, rank, strict)
         path += p
         roots.append(root)
@@ -295,7 +318,57 @@ def partition_path(net: Network, groups: Sequence[Sequence[int]],
     for r in roots[1:]:
         path.append((cur, r))
         cur = st.contract(cur, r)
+    rem = set(later)
+    size = st.net.size
+    while rem:
+        cand = st.neighbours(cur) & rem or rem
+        nxt = min(cand, key=lambda t: (size(st.result(cur, t)), t))
+        rem.discard(nxt)
+        path.append((cur, nxt))
+        cur = st.contract(cur, nxt)
     return path
+
+
+def _sweep_sequence(st: "_State", ids: Sequence[int], rank: Dict[int, int], strict: bool) -> List[int]:
+    """The order in which _linear_on_state would absorb `ids` (first tensor first), computed on
+    a copy of the state."""
+    import copy
+    sc = copy.deepcopy(st)
+    size = sc.net.size
+    remaining = set(ids)
+    first = min(remaining, key=lambda t: rank[t])
+    remaining.discard(first)
+    cur, seq = first, [first]
+    while remaining:
+        cand = sc.neighbours(cur) & remaining
+        if not cand:
+            nxt = min(remaining, key=lambda t: rank[t])
+        elif strict:
+            nxt = min(cand, key=lambda t: rank[t])
+        else:
+            nxt = min(cand, key=lambda t: (size(sc.result(cur, t)), rank[t]))
+        remaining.discard(nxt)
+        seq.append(nxt)
+        cur = sc.contract(cur, nxt)
+    return seq
+
+
+def deferred_search(net: Network, groups: Sequence[Sequence[int]], orders, pre, removed=(),
+                    max_defer: int = 32, step: int = 2) -> Tuple[int, int]:
+    """(defer_left, defer_right) of two-group partition_path minimising the cost model's estimate
+    of an execute (path_info.est_seconds; `removed` = the sliced modes it is priced with)."""
+    best = None
+    for tl in range(0, max_defer + 1, step):
+        for tr in range(0, max_defer + 1, step):
+            try:
+                p = partition_path(net, groups, orders, pre=pre, defer=(tl, tr))
+                info = path_info(net, p, removed)
+            except ValueError:
+                continue
+            key = (info.est_seconds, info.max_size, tl + tr)
+            if best is None or key < best[0]:
+                best = (key, (tl, tr))
+    return best[1] if best else (0, 0)
 
 
 @dataclass

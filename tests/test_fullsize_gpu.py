@@ -2,22 +2,26 @@
 seconds and through size-independent properties where it does not.
 
 * C2 (30q depth-14, one amplitude): the whole network against the oracle.
-* C3 / C4: ONE SLICE of the benchmarked configuration (the same network, path, cut and sliced
-  legs as bench.py: left/right sweeps + the boundary GEMM at K = 2^10 (C3) / 2^16 (C4), i.e. the
-  complex64 LDS-DMA fast GEMM with split-K on C4) against the oracle's exact numpy contraction
+* C3 / C4 / C3d / C4g: ONE SLICE of each configuration (the same network, path, cut and sliced
+  legs as bench.py).  C4 / C3d: left/right sweeps, the slice-invariant boundary GEMM (K = 2^11 /
+  2^8) and the deferred sweep tails absorbed after it per slice (einsum.partition_path
+  defer=...).  C3 / C4g (the plain partition path): the boundary GEMM per slice at K = 2^10 /
+  2^16, C4g's on producer-split f16 planes with split-K.  Against the oracle's exact numpy
+  contraction
   of the same sliced operands (oracle.contract_ref.sliced_operands, the slice enumeration of
   tq_plan_execute).  Normwise bounds (relative to max|amp|): complex64 2e-5, complex128 1e-12.
   Componentwise (the Gauss-3M imaginary part): every amplitude with
   |amp| >= 1e-2 max|amp| within 2e-3 relative, the normwise bound carried down to it.
-* C3 / C4 whole job EXACTLY as bench.py launches it (SlicedContraction at world 1 over the full
-  slice range: C4 4 slice lanes / C3 32, the lane-batched f16-split boundary GEMM with per-lane
-  operand-max words, lane_sum, lane-merged sweep launches, the captured hipGraph replayed)
+* C3 / C3d / C4 / C4g whole job EXACTLY as bench.py launches it (SlicedContraction at world 1
+  over the full slice range: C4 8 slice lanes / C3 and C3d 32 / C4g 4, the f16-split boundary
+  GEMM with operand-max words (C3 / C4g: lane-batched, per-lane words, lane_sum), lane-merged
+  sweep launches, the captured hipGraph replayed)
   against the oracle's sum over all slices (oracle.contract_ref.contract_sliced; the partial sums
   the reference reduces at distributed_engine.py:1477-1497).
 * Lane skew: slices whose operands are 2^36 per cut leg larger than slice 0's, but whose
   contribution is exactly zero, batched in the same lanes as slice 0: the result must be slice
   0's amplitudes at full complex64 accuracy (a scale shared across lanes would flush them).
-* C3 / C4 whole job: sliced + hoisted execution equals the unsliced contraction (2e-5), every
+* C3 / C4 / C3d / C4g whole job: sliced + hoisted execution equals the unsliced contraction (2e-5), every
   4-way rank shard of the slices sums to the full result, and 0 < sum |amp|^2 <= 1 (the
   amplitudes are a sub-block of a unitary circuit's |psi>).
 """
@@ -116,7 +120,8 @@ def _oracle_slice(cfg, sid):
     return _ORACLE_SLICES[key]
 
 
-@pytest.mark.parametrize("cfg,sid", [("C4", 0), ("C4", 5), ("C3", 0), ("C3", 37)])
+@pytest.mark.parametrize("cfg,sid", [("C4", 0), ("C4", 5), ("C3", 0), ("C3", 37), ("C4g", 5),
+                                     ("C3d", 37)])
 @pytest.mark.parametrize("dtype", ["complex64", "complex128"])
 def test_bench_config_slice_vs_oracle(dev, cfg, sid, dtype):
     import torch
@@ -139,7 +144,10 @@ _ORACLE_FULL = {}
 
 
 def _oracle_full(cfg):
-    """Exact (complex128) sum over every slice of config `cfg`, cached per session."""
+    """Exact (complex128) sum over every slice of config `cfg`, cached per session.  C3d / C4g are
+    the same networks as C3 / C4 (same equation and operands, another path): the sum over all
+    slices is the full amplitude block either way, so they share C3's / C4's oracle."""
+    cfg = {"C3d": "C3", "C4g": "C4"}.get(cfg, cfg)
     if cfg not in _ORACLE_FULL:
         from oracle.contract_ref import contract_sliced
         from tneq_qc_amd.circuits import config_task
@@ -163,9 +171,16 @@ def _production_plan_checks(e, cfg, lanes):
     plan = e.plan(torch.complex64)
     assert plan.query("lanes") == lanes, plan.query("lanes")
     d = plan.describe()
+    gemm = [l for l in d.splitlines() if " GEMM " in l]
+    assert len(gemm) == 1 and "amax<-" in gemm[0], gemm
+    if cfg in ("C3d", "C4"):
+        # deferred tails: the boundary GEMM is slice-invariant (run once, fed by its producers'
+        # max words); the slices run only the absorbed tails, lane-merged
+        assert gemm[0].startswith("[once]"), gemm
+        return
     # the lane-batched boundary GEMM fed by its producers' max words, summed over lanes
-    assert " lanes" in d and "lane-sum" in d and "amax<-" in d, d
-    if cfg == "C4":
+    assert " lanes" in d and "lane-sum" in d, d
+    if cfg == "C4g":
         # both halves' per-slice expanding chains as dense ops of one level (tin 16 and 8: one
         # mixed sweepd launch, tq_sweepd.hip)
         dense = [l for l in d.splitlines() if "SWEEP2 DENSE" in l]
@@ -176,7 +191,7 @@ def _production_plan_checks(e, cfg, lanes):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 4)])
+@pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C3d", 32), ("C4", 8), ("C4g", 4)])
 def test_bench_launch_vs_oracle(dev, cfg, lanes):
     import torch
     from tneq_qc_amd.circuits import config_task
@@ -202,7 +217,7 @@ def test_bench_launch_vs_oracle(dev, cfg, lanes):
 
 @pytest.mark.timeout(900)
 def test_planes_gemm_equals_split_kernel(dev):
-    """C4's boundary GEMM on producer-split operands (the dense ops store six f16 term planes
+    """C4g's boundary GEMM on producer-split operands (the dense ops store six f16 term planes
     scaled from a bound of their output; tq_gemmp.hip: Gauss 3M x 3 term products from LDS-DMA
     staged planes, split-K partials, one combine pass summing the lanes) against the same plan on
     the GEMM-side split kernel ("gemm_planes" = 0) and both against the oracle's sum over all
@@ -210,7 +225,7 @@ def test_planes_gemm_equals_split_kernel(dev):
     true max), so they agree to the complex64 tolerance, not bitwise."""
     import torch
     from tneq_qc_amd.circuits import config_task
-    t = config_task("C4")
+    t = config_task("C4g")
     e, ops = _expr_and_ops(t, dev, torch.complex64)
     plan = e.plan(torch.complex64)
     assert plan.query("planes_gemm") == 1
@@ -220,7 +235,7 @@ def test_planes_gemm_equals_split_kernel(dev):
     off = e(*ops).cpu().numpy()
     plan.set("gemm_planes", 1)
     again = e(*ops).cpu().numpy()
-    ref = _oracle_full("C4")
+    ref = _oracle_full("C4g")
     _check(on, ref, TOL["complex64"], "planes")
     _check(off, ref, TOL["complex64"], "split")
     assert np.abs(on - off).max() / np.abs(ref).max() < TOL["complex64"]
@@ -232,7 +247,7 @@ def test_planes_gemm_equals_split_kernel(dev):
     assert np.abs(p1 + p2 - on).max() / np.abs(ref).max() < TOL["complex64"]
 
 
-@pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 4)])
+@pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 8), ("C3d", 32), ("C4g", 4)])
 def test_lane_skew_per_lane_scales(dev, cfg, lanes):
     import torch
     from tneq_qc_amd.circuits import config_task
@@ -262,7 +277,7 @@ def test_lane_skew_per_lane_scales(dev, cfg, lanes):
     _check(got, _oracle_slice(cfg, 0), TOL["complex64"], cfg)
 
 
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
+@pytest.mark.parametrize("cfg", ["C3", "C4", "C3d", "C4g"])
 def test_sliced_equals_unsliced(dev, cfg):
     import torch
     from tneq_qc_amd.circuits import config_task

@@ -234,7 +234,7 @@ def test_gemm_f64_kouter_fast_path(T, dev, dt, M, N, K, B, beta):
 
 
 def test_gemm_c64_bench_shape(T, dev, c64_kernel):
-    """The exact boundary GEMM of the C4 bench (M = N = 1024, K = 65536 per slice, complex64, both
+    """The exact boundary GEMM of the C4g path (C4 before deferred tails) (M = N = 1024, K = 65536 per slice, complex64, both
     operands K-outer; the library splits K 4 ways over the workspace, as in the plan) on random
     operands, against complex128 on a sample of 64 rows (all columns): 2e-5 of max|C|."""
     import tneq_qc_amd._lib as _lib

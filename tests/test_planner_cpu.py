@@ -83,7 +83,7 @@ def test_native_plan_lowering_c1_is_all_apply():
 
 
 def test_native_plan_c4_structure():
-    e, p = _plan(config_task("C4"))
+    e, p = _plan(config_task("C4g"))
     assert p.n_slices == 8
     assert p.query("n_gemm") == 1                        # the boundary GEMM
     d = p.describe().splitlines()
@@ -100,7 +100,7 @@ def test_c4_gemm_operand_max_comes_from_its_producers():
     """The C4 boundary GEMM (complex64, K-outer fast path) reads both operands' max |x| from the
     per-slice sweep ops that store them (csrc/tq_plan.cpp assign_amax), not from a pre-pass."""
     import re
-    e, p = _plan(config_task("C4"))
+    e, p = _plan(config_task("C4g"))
     d = p.describe().splitlines()
     ops = [l for l in d if l.startswith("[once]") or l.startswith("[slice]")]
     gemm = [l for l in ops if "GEMM" in l]
@@ -123,8 +123,8 @@ def _schedule(d):
 
 def test_launch_schedule_covers_every_op_once_and_batches_sweeps():
     """Every op appears in exactly one launch of its set (hoisted / per slice), launches with more
-    than one op hold only independent SWEEP2 ops, and the C4 sweeps share launches."""
-    e, p = _plan(config_task("C4"))
+    than one op hold only independent SWEEP2 ops, and the C4g sweeps share launches."""
+    e, p = _plan(config_task("C4g"))
     d = p.describe().splitlines()
     ops = [l for l in d if l.startswith("[once]") or l.startswith("[slice]")]
     once, per = _schedule(d)
@@ -151,7 +151,7 @@ def test_sweep_tiles_keep_32_columns_on_large_tensors():
     """Tiles with more than 2^(13-5) positions (fewer than 32 columns per chunk) are reserved for
     tensors of at most 2^22 elements (SWEEP2 layout rule, csrc/tq_plan.cpp s2_layout)."""
     import re
-    e, p = _plan(config_task("C4"))
+    e, p = _plan(config_task("C4g"))
     n_wide = 0
     for l in p.describe().splitlines():
         m = re.search(r"SWEEP2 gates=(\d+) tin=(\d+) tout=(\d+) cols=(\d+) C=(\d+)", l)
@@ -215,7 +215,7 @@ def test_sweep2_lane_offsets_stay_32bit(n_legs, want_s2):
     assert ("SWEEP2" in d) == want_s2, d
 
 
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
+@pytest.mark.parametrize("cfg", ["C3", "C4g"])
 def test_boundary_gemm_takes_presplit_operands(cfg):
     """The boundary GEMM of C3 / C4 is a pre-split candidate: both operands come from per-slice
     sweep2 ops that nothing else reads, so those ops may store the f16 terms the GEMM consumes
@@ -223,8 +223,8 @@ def test_boundary_gemm_takes_presplit_operands(cfg):
     e, p = _plan(config_task(cfg))
     gemm = [l for l in p.describe().splitlines() if " GEMM " in l]
     assert len(gemm) == 1 and "amax<-" in gemm[0]
-    if cfg == "C4":
-        # C4's operands come from dense producers, which store the six f16 term planes of the
+    if cfg == "C4g":
+        # C4g's operands come from dense producers, which store the six f16 term planes of the
         # pre-split GEMM instead (tq_gemmp.hip; the planes GEMM replaces the presplit form)
         assert p.query("n_presplit") == 0 and p.query("planes_gemm") == 1 and " planes " in gemm[0]
         assert "planes(A)" in p.describe() and "planes(B)" in p.describe()
@@ -241,7 +241,7 @@ def test_slice_lanes_within_the_arena_budget():
     C4's 1.1-GiB per-slice part gets 4 (the lane copies stay within 6 GiB; tq_plan.cpp, Plan::lanes)."""
     e3, p3 = _plan(config_task("C3"))
     assert p3.query("lanes") == 32
-    e4, p4 = _plan(config_task("C4"))
+    e4, p4 = _plan(config_task("C4g"))
     assert p4.query("lanes") == 4   # 1.1-GiB per-slice part: 4 lanes in the 6-GiB budget
     e2, p2 = _plan(config_task("C2"))
     assert p2.query("lanes") == 1   # one slice
@@ -254,7 +254,7 @@ def test_small_hoisted_levels_run_as_one_chain_launch():
     halves on streams of their own); consecutive ops of a stream hand their tensor over in LDS.
     C2's later 4-chunk levels stay one launch each (measured faster, tq_plan.cpp
     s2_seq_max_chunks); "sweep_chain" = 0 restores one launch per level."""
-    for cfg in ("C2", "C3", "C4"):
+    for cfg in ("C2", "C3", "C4g"):
         e, p = _plan(config_task(cfg))
         d = [l for l in p.describe().splitlines() if l.startswith("# chain launch")]
         assert len(d) == 1 and "<" in d[0] and ">" in d[0], d
@@ -286,11 +286,11 @@ def test_multi_chunk_hoisted_levels_run_as_one_cooperative_launch():
     p.set("sweep_coop", 0)
     assert p.query("n_coop_launches") == 0 and p.query("n_launch_once") == n_on + len(ops) - 1
     p.set("sweep_coop", 1)
-    for cfg in ("C3", "C4"):
+    for cfg in ("C3", "C4g"):
         assert _plan(config_task(cfg))[1].query("n_coop_launches") == 0
 
 
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
+@pytest.mark.parametrize("cfg", ["C3", "C4g"])
 def test_lane_batched_boundary_gemm_and_lane_sum(cfg):
     """With slice lanes the boundary GEMM (lane-local operands) is one batched launch per batch
     (`lanes`), and since only the output permute reads its result the lanes' results are summed
@@ -301,3 +301,41 @@ def test_lane_batched_boundary_gemm_and_lane_sum(cfg):
     assert len(gemm) == 1 and " lanes" in gemm[0] and "lane-sum" in gemm[0]
     perm = [l for l in d if "PERMUTE result->out" in l]
     assert len(perm) == 1 and "[slice]" in perm[0]
+
+
+@pytest.mark.parametrize("cfg,legacy,gain", [("C4", "C4g", 100.0), ("C3d", "C3", 5.0)])
+def test_deferred_tails_shrink_the_boundary(cfg, legacy, gain):
+    """The deferred C3d / C4 paths absorb the last tensors of each half's sweep after the
+    boundary contraction (einsum.partition_path(defer=...)): the boundary GEMM contracts only the
+    cut legs those expanding gates do not touch.  Same network, same amplitudes (GPU parity:
+    tests/test_fullsize_gpu.py); the complex-MAC count drops by `gain` or more and the boundary
+    GEMM becomes slice-invariant (hoisted, run once per execute)."""
+    from tneq_qc_amd import einsum as E
+    t, tg = config_task(cfg), config_task(legacy)
+    assert t.eq == tg.eq and t.path != tg.path
+    net = E.parse_equation(t.eq, t.shapes)
+    E.validate_path(len(net.terms), t.path)
+    f = E.path_info(net, t.path, [net.symbols.index(x) for x in t.sliced]).flops
+    fg = E.path_info(net, tg.path, [net.symbols.index(x) for x in tg.sliced]).flops
+    assert f * gain <= fg, (f, fg)
+    e, p = _plan(t)
+    gemm = [l for l in p.describe().splitlines() if " GEMM " in l]
+    assert len(gemm) == 1 and gemm[0].startswith("[once]"), gemm
+
+
+def test_partition_path_defer_counts():
+    """partition_path(defer=(l, r)) keeps the first len - l (len - r) tensors of each half's sweep,
+    contracts the two half results, then absorbs the deferred tensors; defer=(0, 0) is the plain
+    partition path, and every deferred path is a valid pairwise path of the same network."""
+    from tneq_qc_amd import einsum as E
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task
+    t0 = amplitude_task(BrickWall(12, 6, 0), list(range(4, 8)), cut=6)
+    t1 = amplitude_task(BrickWall(12, 6, 0), list(range(4, 8)), cut=6, defer=(0, 0))
+    assert t0.path == t1.path
+    net = E.parse_equation(t0.eq, t0.shapes)
+    for d in ((2, 0), (0, 3), (4, 4)):
+        t = amplitude_task(BrickWall(12, 6, 0), list(range(4, 8)), cut=6, defer=d)
+        E.validate_path(len(net.terms), t.path)
+        assert t.path != t0.path
+        # the boundary contraction (the step joining the two halves) comes sum(d) steps before the end
+        assert len(t.path) == len(t0.path)

@@ -1,5 +1,5 @@
 """Pre-split boundary-GEMM operands on the GPU (opt-in path) (tq_gemm.hip SplitPre, tq_sweep2.hip f16_terms,
-tq_plan.cpp Op::ps_cand): the per-slice sweep ops that store the two operands of the C3 / C4
+tq_plan.cpp Op::ps_cand): the per-slice sweep ops that store the two operands of the C3 / C4g
 boundary GEMM write them as the f16 terms (h, l) of their values scaled by 2^sc, sc predicted
 from the previous slice's operand max; the GEMM checks the true max against the window
 (max * 2^sc in [2^0, 2^15)) and a slice outside it is re-run on the split path.
@@ -59,7 +59,7 @@ def _split_path(cfg, dev, slice_range=None):
         L.tq_library_set(b"gemm_presplit", 1)
 
 
-# C4's boundary GEMM takes producer-written planes instead (tq_gemmp.hip; test_fullsize_gpu
+# C4g's boundary GEMM takes producer-written planes instead (tq_gemmp.hip; test_fullsize_gpu
 # test_planes_gemm_equals_split_kernel): its plan has no pre-split candidate
 @pytest.mark.parametrize("cfg,rng", [("C3", None), ("C3", (0, 3, 1))])
 def test_presplit_runs_and_matches_split_path(dev, cfg, rng):
