@@ -181,10 +181,22 @@ class Compiler {
         }
       }
     }
-    // ---- branches: the two subtrees of the final step are independent (run concurrently)
-    step_branch_.assign(n_steps, 0);
+    // ---- branches: the two subtrees of the join step are independent (run concurrently, arena
+    // regions of their own); the join and every step outside its subtrees are branch 2 (region
+    // 0).  The join is the step whose smaller subtree holds the most inputs: the final step of a
+    // plain partition path, the boundary contraction when the sweeps' tails are absorbed after
+    // it (einsum.partition_path defer=...)
+    step_branch_.assign(n_steps, 2);
     if (n_steps >= 1) {
-      const int last = n_steps - 1;
+      std::vector<int> leaves(n_inputs + n_steps, 1);
+      int last = n_steps - 1, best = -1;
+      for (int s = 0; s < n_steps; ++s) {
+        const int x = path[2 * s], y = path[2 * s + 1];
+        if (x < 0 || y < 0 || x >= n_inputs + s || y >= n_inputs + s) break;  // checked below
+        leaves[n_inputs + s] = leaves[x] + leaves[y];
+        const int m = std::min(leaves[x], leaves[y]);
+        if (m >= best) { best = m; last = s; }
+      }
       step_branch_[last] = 2;
       for (int side = 0; side < 2; ++side) {
         std::vector<int> stack{path[2 * last + side]};
