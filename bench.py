@@ -4,13 +4,22 @@
 Workload (BASELINE.json metric "amplitudes/sec + achieved MFMA TFLOP/s, 53q depth-20 RQC"):
 config C4 of SURVEY.md §8(d): a 53-qubit depth-20 brick-wall random circuit (520 Haar-random
 2-qubit cores, the reference's build_brick_wall_IM + incidence_to_graph family), |0> inputs,
-33 output bits fixed, 20 open (2^20 correlated bitstrings), cut between qubits 26|27, 3 cut legs
-sliced -> 8 slices.  One "step" = all 2^20 amplitudes: every rank contracts slices
-rank, rank+N, ... (left/right line sweeps + boundary MFMA GEMM, slice-invariant work hoisted)
-into a partial-amplitude buffer, then one RCCL all-reduce (SUM) over xGMI.  Total work is fixed
-as N grows ("scaling": "strong").  Inputs (cores, vectors) are resident in HBM before timing.
-`--config C2 / C3` time the other amplitude configs the same way (C3 = 64 slices, C2 = one
-amplitude, no slicing).
+33 output bits fixed, 20 open (a block of 2^20 correlated bitstrings), cut between qubits 26|27,
+3 cut legs sliced -> 8 slices.  One "step" = one block per rank: left/right line sweeps, the
+boundary MFMA GEMM, the sweeps' deferred tails per slice (slice-invariant work hoisted).
+
+Ranks (`--shard`):
+* bitstrings (default): rank r contracts amplitude block r -- the same network with the closed
+  qubits' fixed bits flipped by r's binary digits (circuits.with_batch), so one compiled plan --
+  over all its slices, with no collective on the data path: per-GPU work is fixed as N grows
+  ("scaling": "weak"; value = N blocks x 2^20 amplitudes / max-over-ranks time).  The same ranks
+  then time ONE block with its slices sharded over them + one RCCL all-reduce (SUM) of the
+  partial amplitudes over xGMI (`slices_strong`, the reference's sliced path,
+  distributed_engine.py:1384-1497).
+* slices: that sliced path as the headline ("scaling": "strong").
+Inputs (cores, vectors) are resident in HBM before timing.
+`--config C2 / C3 / C4g / C3d` time the other amplitude configs the same way (C3 = 64 slices,
+C2 = one amplitude, no slicing; C4g / C3d: other paths of the C4 / C3 networks).
 
 Timing: the headline (`value`, `ms_per_step`) is the production launch path — every step replays
 the plan's captured hipGraph, no events inside.  The dominant kernel's duration (`roofline`) is
@@ -317,6 +326,14 @@ def main():
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C3d", "C4g"],
                     help="C4g: C4 on the big-boundary-GEMM path (each half swept whole); "
                          "C3d: C3 with deferred sweep tails (circuits.config_task)")
+    ap.add_argument("--shard", default="bitstrings", choices=["bitstrings", "slices"],
+                    help="N > 1: bitstrings = rank r contracts its own amplitude block (circuits."
+                         "with_batch: other fixed bits, same plan), no collective (weak scaling); "
+                         "slices = one block, its slices sharded over the ranks + one RCCL all-reduce "
+                         "(strong scaling; also measured as `slices_strong` in bitstrings mode)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="bitstring sharding: rank r contracts block batch + r (tests: a 1-rank run of "
+                         "another rank's block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 training-step line")
     ap.add_argument("--no-alt", action="store_true",
@@ -353,8 +370,14 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    from tneq_qc_amd.circuits import with_batch
+    from tneq_qc_amd.distributed import SlicedContraction
+
     t_plan0 = time.perf_counter()
-    task = config_task(args.config)
+    base = config_task(args.config)
+    bitstrings = args.shard == "bitstrings"
+    # bitstring sharding: rank r's amplitude block r (same network and plan, other fixed bits)
+    task = with_batch(base, args.batch + (rank if bitstrings else 0)) if (bitstrings or args.batch) else base
     expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
     ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
     plan = expr.plan(torch.complex64)
@@ -362,60 +385,101 @@ def main():
     out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
     t_plan = time.perf_counter() - t_plan0
 
-    from tneq_qc_amd.distributed import SlicedContraction
-    job = SlicedContraction(expr)   # slices rank, rank+N, ... + one RCCL all-reduce (SUM)
-    # N > 1: consecutive steps alternate two output buffers and leave their all-reduce in flight
-    # (async): step k's RCCL reduce overlaps step k + 1's contraction, a buffer is reused only after
-    # its reduce has been waited for; the timed region still ends with a device synchronize
-    bufs = [out, torch.empty_like(out)] if world > 1 else [out]
-    works = [None] * len(bufs)
-    nstep = [0]
+    def slices_job():
+        """One block's slices rank, rank+N, ... + one RCCL all-reduce (SUM).  N > 1: consecutive
+        steps alternate two output buffers and leave their all-reduce in flight (async): step k's
+        RCCL reduce overlaps step k + 1's contraction, a buffer is reused only after its reduce has
+        been waited for; the timed region still ends with a device synchronize."""
+        job = SlicedContraction(expr)
+        ops0 = ops if not bitstrings else [torch.from_numpy(o).to(dev, torch.complex64) for o in base.operands]
+        bufs = [out, torch.empty_like(out)] if world > 1 else [out]
+        works = [None] * len(bufs)
+        nstep = [0]
 
-    def step():
-        i = nstep[0] % len(bufs)
-        if world > 1:
-            if works[i] is not None:
-                works[i].wait()
-            _, works[i] = job(*ops, out=bufs[i], async_reduce=True)
-        else:
-            job(*ops, out=out)
-        nstep[0] += 1
+        def step():
+            i = nstep[0] % len(bufs)
+            if world > 1:
+                if works[i] is not None:
+                    works[i].wait()
+                _, works[i] = job(*ops0, out=bufs[i], async_reduce=True)
+            else:
+                job(*ops0, out=out)
+            nstep[0] += 1
 
-    def last_out():
-        for w in works:
-            if w is not None:
-                w.wait()
-        return bufs[(nstep[0] - 1) % len(bufs)]
+        def last():
+            for w in works:
+                if w is not None:
+                    w.wait()
+            return bufs[(nstep[0] - 1) % len(bufs)]
+        return step, last
 
-    def timed(k: int) -> float:
+    if bitstrings:
+        # every rank contracts all slices of its own block: no collective on the data path
+        nstep = [0]
+
+        def step():
+            expr(*ops, out=out)
+            nstep[0] += 1
+
+        def last_out():
+            return out
+    else:
+        step, last_out = slices_job()
+
+    def timed(k: int, fn=None) -> float:
+        fn = fn or step
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(k):
-            step()
+            fn()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     _log(f"plan compiled in {t_plan:.1f} s ({n_slices} slices); warmup")
     for _ in range(args.warmup):
         step()
     # ---- headline: production path (hipGraph replay per step, no events)
-    dt = timed(args.steps)
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(timed(args.steps))
     graphs = plan.query("graph_launches")
     if args.save_out:
         res = last_out()
+        import numpy as np
         if rank == 0:
-            import numpy as np
             np.save(args.save_out, res.cpu().numpy())
+        elif bitstrings:   # every rank's own block (tests check each against the 1-rank blocks)
+            root, ext = os.path.splitext(args.save_out)
+            np.save(f"{root}.rank{rank}{ext}", res.cpu().numpy())
+    slices_strong = None
+    if bitstrings and world > 1:
+        # the same ranks on ONE block, its slices sharded + the RCCL all-reduce (strong scaling)
+        s_step, s_last = slices_job()
+        for _ in range(args.warmup):
+            s_step()
+        dts = max_over_ranks(timed(args.steps, s_step))
+        res_s = s_last()
+        if args.save_out and rank == 0:
+            import numpy as np
+            root, ext = os.path.splitext(args.save_out)
+            np.save(f"{root}.slices{ext}", res_s.cpu().numpy())
+        slices_strong = {"value": base.n_amplitudes * args.steps / dts, "unit": "amplitudes/s",
+                         "ms_per_step": dts / args.steps * 1e3, "scaling": "strong",
+                         "parallelism": f"slices{world}", "slices_per_rank": len(range(rank, n_slices, world)),
+                         "collective": f"RCCL all-reduce (SUM) of the {base.n_amplitudes}-amplitude partials"
+                                       if args.dist_backend == "nccl" else "gloo all-reduce (SUM)"}
+        _log(f"slices (strong) on one block: {dts / args.steps * 1e3:.2f} ms/step")
 
     _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step")
     # ---- dominant kernel: the same K steps launched eagerly with HIP events around every GEMM
@@ -431,7 +495,7 @@ def main():
     kinds = {k: plan.profile_read(getattr(_lib, f"TQ_OP_{k}")) for k in ("APPLY", "SWEEP", "PERMUTE", "GEMM")}
     plan.profile(None)
 
-    n_amp = task.n_amplitudes
+    n_amp = task.n_amplitudes * (world if bitstrings else 1)   # amplitudes of the whole job per step
     L = _lib.lib()
     g3m = bool(L.tq_library_query(b"gemm_3m") == 1)
     bf16 = bool(L.tq_library_query(b"gemm_bf16") == 1)
@@ -494,20 +558,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if args.shard == "bitstrings" else "strong",
         "vs_baseline": None,
         "dtype": "c64",
         "data": "synthetic (Haar-random 2-qubit cores, seeded; |0> inputs; seeded fixed bits)",
         "config": {
-            "workload": f"{args.config}: {task.circuit.n_qubits}q depth-{task.circuit.depth} brick-wall RQC, "
-                        f"{n_amp} correlated amplitudes ({len(task.open_qubits)} open), cut {task.cut}, "
-                        f"{n_slices} slices ({len(task.sliced)} sliced cut legs) over {world} GPU(s), RCCL all-reduce",
+            "workload": (f"{args.config}: {task.circuit.n_qubits}q depth-{task.circuit.depth} brick-wall RQC, "
+                         f"{task.n_amplitudes} correlated amplitudes per block ({len(task.open_qubits)} open), "
+                         f"cut {task.cut}, {n_slices} slices ({len(task.sliced)} sliced cut legs); "
+                         + (f"{world} GPU(s), one block per rank (bitstring sharding, no collective)" if bitstrings
+                            else f"{world} GPU(s), slices sharded, RCCL all-reduce")),
             "n_qubits": task.circuit.n_qubits,
             "depth": task.circuit.depth,
             "amplitudes_per_step": n_amp,
+            "amplitudes_per_block": task.n_amplitudes,
+            "blocks_per_step": world if bitstrings else 1,
             "slices": n_slices,
-            "parallelism": f"slices{world}",
-            "slices_per_rank": len(range(rank, n_slices, world)),
+            "parallelism": f"bitstrings{world}" if bitstrings else f"slices{world}",
+            "slices_per_rank": n_slices if bitstrings else len(range(rank, n_slices, world)),
         },
         "timing": {
             "headline": "hipGraph replay of the whole plan per step (production path), no events",
@@ -584,6 +652,8 @@ def main():
             res["roofline"]["traffic_unit"] = "bytes per step (sweep launches)"
             res["roofline"]["traffic_vs_algorithmic"] = per * sweep_["launches"] / max(1.0, sweep_["bytes"])
             res["roofline"]["traffic_source"] = f"profiles/{src}"
+    if slices_strong:
+        res["slices_strong"] = slices_strong
     if rank == 0:
         _log("permute probe")
         try:

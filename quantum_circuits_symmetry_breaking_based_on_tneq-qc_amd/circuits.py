@@ -287,9 +287,12 @@ def diamond_order(circ: BrickWall, kinds, net: Network, ids: Sequence[int], upwa
 
 # ---- the BASELINE.json configurations ------------------------------------------------------
 
-def config_task(name: str, seed: int = 0) -> AmplitudeTask:
+def config_task(name: str, seed: int = 0, batch: int = 0) -> AmplitudeTask:
     """C1..C4 amplitude workloads; C5 is the symmetry-breaking ansatz
-    (see ansatz_qctn)."""
+    (see ansatz_qctn).  `batch` selects another block of amplitudes of the same network
+    (amplitude_task: other fixed bits, same plan) -- bench.py's bitstring sharding."""
+    if batch:
+        return with_batch(config_task(name, seed), batch)
     if name == "C1":   # 10q d8, one amplitude (CPU plumbing config)
         return amplitude_task(BrickWall(10, 8, seed), [])
     if name == "C2":   # 30q d14, one amplitude, no slicing
@@ -308,6 +311,28 @@ def config_task(name: str, seed: int = 0) -> AmplitudeTask:
         # (per slice a 1024 x 1024 x 65536 complex GEMM fed by the dense sweeps: the big-GEMM path)
         return amplitude_task(BrickWall(53, 20, seed), list(range(17, 37)), cut=27, n_slice=3)
     raise ValueError(f"unknown config {name!r}")
+
+
+def with_batch(task: AmplitudeTask, batch: int) -> AmplitudeTask:
+    """Amplitude block `batch` of the same network: the closed qubits' fixed bits with the lowest
+    ones flipped by the binary digits of `batch` (blocks b != b' hold disjoint bitstrings), i.e.
+    only the output projector operands change -- equation, shapes, path and slicing are the
+    task's own, so one compiled plan serves every block (bench.py's bitstring sharding)."""
+    import dataclasses
+    closed = sorted(task.fixed_bits)
+    if not 0 <= batch < 2 ** len(closed):
+        raise ValueError(f"batch {batch} out of range for {len(closed)} closed qubits")
+    bits = dict(task.fixed_bits)
+    for i, q in enumerate(closed):
+        if (batch >> i) & 1:
+            bits[q] ^= 1
+    ops = list(task.operands)
+    for i, (kind, q) in enumerate(task.kinds):
+        if kind == "proj":
+            e = np.zeros(2, dtype=np.complex128)
+            e[bits[q]] = 1.0
+            ops[i] = e
+    return dataclasses.replace(task, operands=ops, fixed_bits=bits)
 
 
 TRAIN_MASK = [2, 3, 5, 8, 9, 12, 13, 14, 15, 17, 18, 20, 21, 23, 25, 26, 29, 31, 32, 33]  # train.py:30

@@ -218,3 +218,70 @@ def test_more_ranks_than_slices_gradients():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     for rank, e_out, e_g in sorted(q.get(timeout=5) for _ in range(3)):
         assert e_out < 1e-12 and e_g < 1e-10, (rank, e_out, e_g)
+
+
+def test_bitstring_blocks_partition_the_state():
+    """bench.py's bitstring sharding (circuits.with_batch): block b fixes the closed qubits to the
+    base bits flipped by b's binary digits -- the same equation, shapes, path and slicing (one
+    plan for every block), only the projector operands differ; a fresh amplitude_task with those
+    bits builds the same operands; and the 2^closed blocks are disjoint and cover the state:
+    sum over every block of sum |amp|^2 = 1 (a unitary circuit on |0...0>)."""
+    from oracle.contract_ref import contract_sliced
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task, with_batch
+    circ = BrickWall(9, 4, 3)
+    opn = list(range(3, 7))
+    t = amplitude_task(circ, opn, cut=4, n_slice=2, defer=(2, 2))
+    n_closed = len(t.fixed_bits)
+    total = 0.0
+    seen = set()
+    for b in range(2 ** n_closed):
+        tb = with_batch(t, b)
+        assert tb.eq == t.eq and tb.shapes == t.shapes and tb.path == t.path and tb.sliced == t.sliced
+        bits = tuple(sorted(tb.fixed_bits.items()))
+        assert bits not in seen
+        seen.add(bits)
+        if b in (0, 1, 2 ** n_closed - 1):
+            fresh = amplitude_task(circ, opn, fixed_bits=tb.fixed_bits, cut=4, n_slice=2, defer=(2, 2))
+            assert fresh.eq == tb.eq
+            assert all(np.array_equal(x, y) for x, y in zip(fresh.operands, tb.operands))
+        amp = contract_sliced(tb.eq, tb.operands, tb.sliced, tb.path)
+        total += float((np.abs(amp) ** 2).sum())
+    assert abs(total - 1.0) < 1e-10, total
+    with pytest.raises(ValueError):
+        with_batch(t, 2 ** n_closed)
+
+
+def _bitstring_worker(rank, world, port, q):
+    """bench.py --shard bitstrings on CPU: rank r contracts block r on its own (no collective on
+    the data path); the test gathers the blocks only to check them."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle.contract_ref import contract_sliced
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task, with_batch
+    base = amplitude_task(BrickWall(12, 6, 2), list(range(4, 8)), cut=6, n_slice=3)
+    mine = with_batch(base, rank)
+    amp = torch.from_numpy(contract_sliced(mine.eq, mine.operands, mine.sliced, mine.path))
+    got = [torch.zeros_like(amp) for _ in range(world)]
+    dist.all_gather(got, amp)
+    if rank == 0:
+        err = 0.0
+        for r in range(world):
+            tr = with_batch(base, r)
+            ref = contract_sliced(tr.eq, tr.operands, tr.sliced, tr.path)
+            err = max(err, float(np.abs(got[r].numpy() - ref).max() / np.abs(ref).max()))
+        q.put(err)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_bitstring_blocks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bitstring_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) == 0.0
