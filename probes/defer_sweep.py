@@ -2,7 +2,7 @@
 replayed) of a config's network over several deferred-tail splits (einsum.partition_path
 defer=(left, right)), and check every split gives the same amplitudes.
 
-    python probes/defer_sweep.py C3 0,0 4,4 10,8 ...
+    python probes/defer_sweep.py C3 [ns=K] 0,0 4,4 10,8 ...     (ns: sliced cut legs, default the config's)
 """
 import sys
 import time
@@ -28,7 +28,11 @@ def main():
     circ, opn, cut, ns = ARGS[cfg]
     dev = torch.device("cuda:0")
     ref = None
-    for spec in sys.argv[2:]:
+    specs = sys.argv[2:]
+    if specs and specs[0].startswith("ns="):
+        ns = int(specs[0][3:])
+        specs = specs[1:]
+    for spec in specs:
         d = tuple(int(x) for x in spec.split(","))
         t = amplitude_task(circ, opn, cut=cut, n_slice=ns, defer=d)
         net = E.parse_equation(t.eq, t.shapes)

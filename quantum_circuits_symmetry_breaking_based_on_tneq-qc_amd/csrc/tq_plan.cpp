@@ -266,10 +266,14 @@ class Compiler {
           op.note += " lanes";
           wsmax = std::max(wsmax, gemm_workspace(P_.dtype, op.M, op.N, op.K, P_.lanes));
         }
-        // a lane-batched GEMM whose result only an output permute reads: sum the lanes first
+        // a lane-batched GEMM or a lane-merged sweep2 level (a per-slice op: every lane's copy in
+        // one launch) whose result only an output permute reads: sum the lanes first, then permute
+        // once per batch instead of once per lane
         for (size_t i = 0; i < P_.ops.size(); ++i) {
           Op& g = P_.ops[i];
-          if (!g.lane_batch) continue;
+          const bool s2 = g.kind == OP_SWEEP2 && !g.s2_dense && !g.invariant && !g.writes_output &&
+                          g.c.kind == BUF_ARENA;
+          if (!g.lane_batch && !s2) continue;
           const int64_t lo = g.c.off, hi = g.c.off + g.nc;
           int reader = -1, nread = 0;
           for (size_t k = i + 1; k < P_.ops.size(); ++k) {
@@ -3262,6 +3266,13 @@ int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin,
       if (merged || lane_sl.size() == 1) {
         set_lane(0);
         TQ_TRY(launch(grp));
+        if (merged && lane_sl.size() > 1)
+          for (int j : grp)
+            if (P.ops[j].lane_sum) {   // a lane-merged level whose lanes an output permute sums
+              TQ_TRY(lane_sum_launch(P.dtype, P.ops[j].nc, ptr(P.ops[j].c), (int64_t)(P.lane_stride / esz),
+                                     (int)lane_sl.size(), stream));
+              lanes_summed = true;
+            }
       } else if (op0.kind == OP_GEMM && op0.lane_batch) {
         set_lane(0);
         lane_gemm = (int)lane_sl.size();
