@@ -931,7 +931,12 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   if (amax) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(vmax));
+    // one atomic per wave only when it raises the word: every wave of a big op finishes at about
+    // the same time, and thousands of same-address atomics serialise in one L2 channel (a 2^21-
+    // element operand took 58 us); a relaxed read first skips the ones that cannot win
+    if ((threadIdx.x & 63) == 0 &&
+        __float_as_uint(vmax) > __hip_atomic_load(amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(amax, __float_as_uint(vmax));
   }
 #ifdef TQ_S2_TIMING
   __builtin_amdgcn_s_waitcnt(0);

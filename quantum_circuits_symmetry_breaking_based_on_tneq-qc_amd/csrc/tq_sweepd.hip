@@ -429,7 +429,9 @@ __device__ __forceinline__ void sweepd_op(const S2DOp& op, SdSmem<TMAX>& sm) {
   if (track) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-    if (lane == 0) atomicMax(op.amax, __float_as_uint(vmax));
+    if (lane == 0 &&   // only when it raises the word (same-address atomics serialise: tq_sweep2.hip)
+        __float_as_uint(vmax) > __hip_atomic_load(op.amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(op.amax, __float_as_uint(vmax));
   }
 }
 
