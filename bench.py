@@ -331,6 +331,10 @@ def main():
                          "with_batch: other fixed bits, same plan), no collective (weak scaling); "
                          "slices = one block, its slices sharded over the ranks + one RCCL all-reduce "
                          "(strong scaling; also measured as `slices_strong` in bitstrings mode)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="bitstring sharding: blocks in flight per GPU -- M plans (own arenas), step k "
+                         "on plan k %% M's stream (each step one whole block; the sweeps are latency-"
+                         "bound, so a second block fills the idle CUs); 1 = one stream")
     ap.add_argument("--batch", type=int, default=0,
                     help="bitstring sharding: rank r contracts block batch + r (tests: a 1-rank run of "
                          "another rank's block)")
@@ -413,15 +417,31 @@ def main():
             return bufs[(nstep[0] - 1) % len(bufs)]
         return step, last
 
+    def step1():
+        """One block on the current stream (plan 0): the latency pass and the profiled passes."""
+        expr(*ops, out=out)
+
+    inflight = max(1, args.inflight) if bitstrings else 1
     if bitstrings:
-        # every rank contracts all slices of its own block: no collective on the data path
+        # every rank contracts all slices of its own blocks: no collective on the data path.  Slot i
+        # of rank r holds block batch + r + N*i (its own plan, arena, operands and stream); step k
+        # runs on slot k % inflight, so up to `inflight` blocks are in flight on the GPU
+        slots = [(expr, ops, out, torch.cuda.current_stream(dev))]
+        for i in range(1, inflight):
+            ti = with_batch(base, args.batch + rank + world * i)
+            ei = HipContractExpression(ti.eq, *ti.shapes, optimize=ti.path, slices=ti.sliced)
+            slots.append((ei, [torch.from_numpy(o).to(dev, torch.complex64) for o in ti.operands],
+                          torch.empty(ei.out_shape, dtype=torch.complex64, device=dev), torch.cuda.Stream(dev)))
         nstep = [0]
 
         def step():
-            expr(*ops, out=out)
+            e_i, ops_i, out_i, s_i = slots[nstep[0] % inflight]
+            with torch.cuda.stream(s_i):
+                e_i(*ops_i, out=out_i)
             nstep[0] += 1
 
         def last_out():
+            torch.cuda.synchronize()
             return out
     else:
         step, last_out = slices_job()
@@ -481,16 +501,19 @@ def main():
                                        if args.dist_backend == "nccl" else "gloo all-reduce (SUM)"}
         _log(f"slices (strong) on one block: {dts / args.steps * 1e3:.2f} ms/step")
 
-    _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step")
-    # ---- dominant kernel: the same K steps launched eagerly with HIP events around every GEMM
+    _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step ({inflight} in flight)")
+    # ---- one block at a time (one stream): the latency of a step
+    dt_lat = max_over_ranks(timed(args.steps, step1)) if inflight > 1 else dt
+    # ---- dominant kernel: the same K steps launched eagerly (one stream) with HIP events around
+    # every GEMM
     plan.profile(_lib.TQ_OP_GEMM)
-    dt_prof = timed(args.steps)
+    dt_prof = timed(args.steps, step1)
     gemm = plan.profile_read(_lib.TQ_OP_GEMM)
     plan.profile(None)
 
     # ---- one profiled step for the HBM-bound kernels (evidence for DESIGN.md)
     plan.profile(-1)
-    step()
+    step1()
     torch.cuda.synchronize()
     kinds = {k: plan.profile_read(getattr(_lib, f"TQ_OP_{k}")) for k in ("APPLY", "SWEEP", "PERMUTE", "GEMM")}
     plan.profile(None)
@@ -578,9 +601,14 @@ def main():
             "slices_per_rank": n_slices if bitstrings else len(range(rank, n_slices, world)),
         },
         "timing": {
-            "headline": "hipGraph replay of the whole plan per step (production path), no events",
+            "headline": ("hipGraph replay of the whole plan per step (production path), no events"
+                         + (f"; {inflight} blocks in flight per GPU (step k on plan k mod {inflight}'s stream, "
+                            f"each step one whole block)" if inflight > 1 else "")),
             "graph_launches_timed": graphs,
             "eager_profiled_ms_per_step": dt_prof / args.steps * 1e3,
+            "inflight": inflight,
+            "latency_ms_per_step": dt_lat / args.steps * 1e3,
+            "latency_definition": "the same K steps one block at a time on one stream (no overlap of steps)",
         },
         "roofline": {
             "bound": "mfma",

@@ -1224,10 +1224,13 @@ class Compiler {
     }();
     return v;
   }
+  // chunks a big sweep2 op is split into at least (TQ_S2_MINCHUNKS): 128 since r05 (the deferred
+  // C4 path's 2^19-element levels, two halves per launch: 0.766 -> 0.747 ms per block, two blocks
+  // in flight 0.565 -> 0.520; C2 / C3 +-0; 64 / 512: 0.80 / 0.88, profiles/knobs_r05.txt)
   static int s2_min_chunks() {
     static const int v = [] {
       const char* e = getenv("TQ_S2_MINCHUNKS");
-      return e ? atoi(e) : 256;
+      return e ? atoi(e) : 128;
     }();
     return v;
   }
