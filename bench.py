@@ -22,10 +22,11 @@ Inputs (cores, vectors) are resident in HBM before timing.
 C2 = one amplitude, no slicing; C4g / C3d: other paths of the C4 / C3 networks).
 
 Timing: the headline (`value`, `ms_per_step`) is the production launch path — every step replays
-the plan's captured hipGraph, no events inside.  The dominant kernel's duration (`roofline`) is
-then measured in a separate pass of the same K steps in which the plan launches eagerly with HIP
-events around every GEMM launch on its stream (the kernels are identical; rocprofv3's average
-for the same command is committed under profiles/).
+the plan's captured hipGraph, no events inside (two blocks in flight, see above).  The dominant
+kernel's duration (`roofline`) is then measured in separate single-stream passes of the same steps
+in which the plan launches eagerly with HIP events around every launch of that kernel kind on its
+stream (the kernels are identical); rocprofv3's average for the same command, committed under
+profiles/, is reported beside it (`*_rocprof`).
 
 Prints ONE JSON line on rank 0 with `roofline` and, at N=1, `cpu_baseline` (the oracle's numpy
 pairwise executor on a bounded sample of the same network, in the same dtype).
@@ -74,6 +75,22 @@ def _profile_json(name: str, config: str):
     except Exception:
         pass
     return None
+
+
+def _rocprof_avg_ns(name: str, kernel: str):
+    """Average duration (ns) over every dispatch of kernels whose name contains `kernel` in a
+    committed rocprofv3 --stats CSV under profiles/ (or None)."""
+    import csv
+    try:
+        calls, tot = 0, 0.0
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            for r in csv.DictReader(f):
+                if kernel in r["Name"]:
+                    calls += int(r["Calls"])
+                    tot += float(r["TotalDurationNs"])
+        return tot / calls if calls else None
+    except Exception:
+        return None
 
 
 def _cgroup_cpu_max():
@@ -569,6 +586,14 @@ def main():
                     else "4 real f32 MFMA GEMMs per complex GEMM") + ")")
         exe_def = "executed MFMA flops per launch (3M: 6*M*N*K, 4M: 8*M*N*K real) / avg launch time"
     clk = (pmc_b or {}).get("effective_clock_GHz")
+    gemm_rp = None
+    if planes and args.config == "C4g":
+        # rocprofv3 average of the same launch (GEMM + combine) from the committed kernel stats of
+        # this path's bench command (r05, when it was the C4 default)
+        g_ns = _rocprof_avg_ns("rocprof_r05_bench_kernel_stats.csv", "gemm_planes_kernel")
+        c_ns = _rocprof_avg_ns("rocprof_r05_bench_kernel_stats.csv", "planes_combine_kernel")
+        if g_ns and c_ns:
+            gemm_rp = (g_ns + c_ns) / 1e6
     apply_ = kinds["APPLY"]
     sweep_ = kinds["SWEEP"]
     perm_ = kinds["PERMUTE"]
@@ -625,6 +650,8 @@ def main():
             "mfma_busy_pmc": (pmc_b or {}).get("mfma_busy_frac"),
             "traffic": (pmc_t or {}).get("hbm_bytes_per_launch"),
             "avg_launch_ms": avg_gemm_s * 1e3,
+            "avg_launch_ms_rocprof": gemm_rp,
+            "frac_rocprof": (exe_flops / (gemm_rp / 1e3) / 1e12 / peak) if gemm_rp else None,
             "flops_per_launch_algorithmic": alg_flops,
             "flops_per_launch_executed": exe_flops,
             "launches_timed": gemm["launches"],
@@ -667,6 +694,16 @@ def main():
             "ms_per_step": sweep_["ms"],
             "algorithmic_bytes_per_step": sweep_["bytes"],
         }
+        # rocprofv3 kernel stats of the default bench command (scripts/prof_round.sh r05f): the
+        # average sweep2 launch there, priced with this step's algorithmic bytes per launch
+        st = _rocprof_avg_ns("rocprof_r05f_bench_kernel_stats.csv", "sweep2_kernel") if args.config == "C4" else None
+        if st and sweep_["launches"]:
+            per_launch = sweep_["bytes"] / sweep_["launches"]
+            res["roofline"]["avg_launch_us_events"] = sweep_["ms"] / sweep_["launches"] * 1e3
+            res["roofline"]["avg_launch_us_rocprof"] = st / 1e3
+            res["roofline"]["achieved_rocprof"] = per_launch / (st / 1e9) / 1e9
+            res["roofline"]["frac_rocprof"] = res["roofline"]["achieved_rocprof"] / PEAK_HBM_GBS
+            res["roofline"]["rocprof_source"] = "profiles/rocprof_r05f_bench_kernel_stats.csv (sweep2_kernel, all forms)"
         src = f"pmc_{args.config.lower()}_r05.json"
         pmc_s = _profile_json(src, args.config)
         if not pmc_s:

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Phase timing of every sweep2 op of one C4 execute (development aid).  Needs libtneqhip.so
-built with -DTQ_S2_TIMING (make EXTRA=-DTQ_S2_TIMING): workgroup 0 of each op stamps the wall
+built with -DTQ_S2_TIMING (csrc: make BUILD=../lib/obj_timing OUT=../lib/libtneqhip_timing.so EXTRA=-DTQ_S2_TIMING): workgroup 0 of each op stamps the wall
 clock (100 MHz) at: start, descriptor staged, tables built, first chunk in LDS, first chunk's
 gates done, first chunk stored, end.  Prints per-op phase durations in us.
     TNEQHIP_LIB=<timing build> python scripts/sweep_timing.py [C4|C3|C2] [slices]"""
