@@ -694,6 +694,25 @@ def main():
             "ms_per_step": sweep_["ms"],
             "algorithmic_bytes_per_step": sweep_["bytes"],
         }
+        if sweep_["ms"] and sweep_["flops"]:
+            # the same launches against the FP32 vector roof: the gate arithmetic (complex MACs x 8
+            # flops, tq_plan.cpp emit_s2) over the same event time; arithmetic intensity vs the
+            # ridge point says which roof binds (above the ridge: VALU, below: HBM)
+            tf = sweep_["flops"] / (sweep_["ms"] / 1e3) / 1e12
+            ai = sweep_["flops"] / max(1.0, sweep_["bytes"])
+            ridge = PEAK_FP32_MFMA_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+            attain = min(PEAK_FP32_MFMA_TFLOPS, ai * PEAK_HBM_GBS / 1e3)   # TFLOP/s
+            res["roofline"].update({
+                "flops_per_step_algorithmic": sweep_["flops"],
+                "achieved_tflops": tf,
+                "valu_fp32_peak_tflops": PEAK_FP32_MFMA_TFLOPS,
+                "frac_valu": tf / PEAK_FP32_MFMA_TFLOPS,
+                "arith_intensity_flop_per_byte": ai,
+                "ridge_flop_per_byte": ridge,
+                "frac_of_attainable": tf / attain,
+                "attainable_definition": "min(FP32 vector peak, intensity x 8 TB/s): the roof that binds "
+                                         "at this arithmetic intensity (sweep2 is latency-bound under both)",
+            })
         # rocprofv3 kernel stats of the default bench command (scripts/prof_round.sh r05f): the
         # average sweep2 launch there, priced with this step's algorithmic bytes per launch
         st = _rocprof_avg_ns("rocprof_r05f_bench_kernel_stats.csv", "sweep2_kernel") if args.config == "C4" else None
