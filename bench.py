@@ -340,9 +340,10 @@ def main():
     ap.add_argument("--save-out", default=None, help="rank 0 saves the last step's amplitudes (.npy)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C3d", "C4g"],
+    ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C3d", "C4g", "C4x4"],
                     help="C4g: C4 on the big-boundary-GEMM path (each half swept whole); "
-                         "C3d: C3 with deferred sweep tails (circuits.config_task)")
+                         "C3d: C3 with deferred sweep tails; C4x4: 4 C4 blocks per contraction "
+                         "(circuits.config_task)")
     ap.add_argument("--shard", default="bitstrings", choices=["bitstrings", "slices"],
                     help="N > 1: bitstrings = rank r contracts its own amplitude block (circuits."
                          "with_batch: other fixed bits, same plan), no collective (weak scaling); "
@@ -766,7 +767,8 @@ def main():
                 res[key] = {"error": repr(e)}
     if world == 1 and rank == 0 and args.config == "C4" and not args.no_other:
         # C4g: the same amplitudes on the big-boundary-GEMM path (the planes GEMM's roofline)
-        for cfg in ("C2", "C3", "C4g"):
+        # C4x4: 4 blocks of C4 in one contraction (2^22 amplitudes; a larger correlated batch)
+        for cfg in ("C2", "C3", "C4g", "C4x4"):
             _log(f"secondary config {cfg}")
             try:
                 res[f"config_{cfg}"] = other_config(args, cfg)

@@ -307,6 +307,16 @@ def config_task(name: str, seed: int = 0, batch: int = 0) -> AmplitudeTask:
         # the last 20 / 16 tensors of the two sweeps absorbed after the boundary contraction
         # (einsum.deferred_search on this network: 5.6e11 -> 3.5e9 complex MACs per execute)
         return amplitude_task(BrickWall(53, 20, seed), list(range(17, 37)), cut=27, n_slice=3, defer=(20, 16))
+    if name == "C4x4":  # C4's network with qubits 16 and 37 open too: 4 blocks of C4 in one contraction
+        # (2^22 amplitudes; C4's fixed bits elsewhere, so the (q16, q37) = C4's-bits sub-block IS C4's
+        # block).  Larger correlated batches amortise the hoisted sweeps: 0.32 ms per 2^20 amplitudes
+        # on one stream against C4's 0.74 (profiles/open_batch_r05.txt)
+        rng = np.random.default_rng(7)
+        bits = {q: int(rng.integers(0, 2)) for q in range(53) if not 17 <= q < 37}
+        bits.pop(16)
+        bits.pop(37)
+        return amplitude_task(BrickWall(53, 20, seed), list(range(16, 38)), fixed_bits=bits, cut=27, n_slice=3,
+                              defer=(20, 16))
     if name == "C4g":  # C4 on the r02-r05 path: each half swept whole, then ONE boundary contraction
         # (per slice a 1024 x 1024 x 65536 complex GEMM fed by the dense sweeps: the big-GEMM path)
         return amplitude_task(BrickWall(53, 20, seed), list(range(17, 37)), cut=27, n_slice=3)

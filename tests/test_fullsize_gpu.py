@@ -296,3 +296,23 @@ def test_sliced_equals_unsliced(dev, cfg):
     assert err2 < TOL["complex64"], err2
     p = (full.abs() ** 2).sum().item()
     assert 0.0 < p <= 1.0 + 1e-4
+
+
+def test_c4x4_holds_the_c4_block(dev):
+    """C4x4 (bench secondary line): the C4 network with qubits 16 and 37 open too, C4's fixed bits
+    elsewhere -- one contraction of 4 blocks.  Its (q16, q37) = C4's-bits sub-block must be C4's
+    amplitudes (C4 itself is checked against the oracle above), and 0 < sum |amp|^2 <= 1."""
+    import torch
+    from tneq_qc_amd.circuits import config_task
+    t4, t = config_task("C4x4"), config_task("C4")
+    e4, ops4 = _expr_and_ops(t4, dev, torch.complex64)
+    e, ops = _expr_and_ops(t, dev, torch.complex64)
+    big = e4(*ops4).cpu().numpy()
+    ref = e(*ops).cpu().numpy()
+    idx = tuple(t.fixed_bits[q] if q in (16, 37) else slice(None) for q in t4.open_qubits)
+    assert [q for q in t4.open_qubits if q not in (16, 37)] == t.open_qubits
+    sub = big[idx]
+    assert sub.shape == ref.shape
+    assert np.abs(sub - ref).max() / np.abs(ref).max() < TOL["complex64"]
+    p = float((np.abs(big) ** 2).sum())
+    assert 0.0 < p <= 1.0 + 1e-4
