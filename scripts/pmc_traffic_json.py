@@ -26,7 +26,7 @@ def counter(cfg, c):
     return tot, len(disp), len(sgdg)
 
 
-for cfg in ("C2", "C3", "C4"):
+for cfg in ("C2", "C3", "C4", "C4x4"):
     fk, fd, _ = counter(cfg, "FETCH_SIZE")
     wk, wd, _ = counter(cfg, "WRITE_SIZE")
     if not fd:
