@@ -339,3 +339,28 @@ def test_partition_path_defer_counts():
         assert t.path != t0.path
         # the boundary contraction (the step joining the two halves) comes sum(d) steps before the end
         assert len(t.path) == len(t0.path)
+
+
+def test_deferred_paths_contract_to_the_same_amplitudes():
+    """Every deferred split of a small cut network is a valid pairwise path of the same network and
+    the oracle's contraction along it gives the plain partition path's amplitudes (sliced sums
+    included); einsum.deferred_search's pick costs no more than the plain path in the model."""
+    import numpy as np
+    from oracle.contract_ref import contract_sliced
+    from tneq_qc_amd import einsum as E
+    from tneq_qc_amd.circuits import BrickWall, amplitude_task
+    circ = BrickWall(12, 6, 4)
+    t0 = amplitude_task(circ, list(range(4, 8)), cut=6, n_slice=2)
+    ref = contract_sliced(t0.eq, t0.operands, t0.sliced, t0.path)
+    net = E.parse_equation(t0.eq, t0.shapes)
+    for d in ((2, 2), (4, 0), (0, 4), (6, 6)):
+        t = amplitude_task(circ, list(range(4, 8)), cut=6, n_slice=2, defer=d)
+        assert t.eq == t0.eq
+        E.validate_path(len(net.terms), t.path)
+        got = contract_sliced(t.eq, t.operands, t.sliced, t.path)
+        assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), d
+    ta = amplitude_task(circ, list(range(4, 8)), cut=6, n_slice=2, defer="auto")
+    sl = lambda t: [net.symbols.index(x) for x in t.sliced]
+    assert E.path_info(net, ta.path, sl(ta)).est_seconds <= E.path_info(net, t0.path, sl(t0)).est_seconds * (1 + 1e-9)
+    got = contract_sliced(ta.eq, ta.operands, ta.sliced, ta.path)
+    assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
