@@ -364,3 +364,23 @@ def test_deferred_paths_contract_to_the_same_amplitudes():
     assert E.path_info(net, ta.path, sl(ta)).est_seconds <= E.path_info(net, t0.path, sl(t0)).est_seconds * (1 + 1e-9)
     got = contract_sliced(ta.eq, ta.operands, ta.sliced, ta.path)
     assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+def test_branches_follow_the_boundary_join():
+    """With deferred tails the final step joins a tail gate, not the two halves: the plan's two
+    branches (own arena regions, tq_plan.cpp branches pre-pass) must still be the halves, so their
+    hoisted sweep levels share launches (C4: most hoisted launches hold one op of each half)."""
+    e, p = _plan(config_task("C4"))
+    d = p.describe().splitlines()
+    ops = [l for l in d if l.startswith("[once]") or l.startswith("[slice]")]
+    assert any(" b0 " in l for l in ops) and any(" b1 " in l for l in ops)
+    pairs = 0
+    for l in d:
+        if l.startswith("# once"):
+            ids = [int(x) for x in l.split()[2:]]
+            br = {ops[i].split()[1] for i in ids}
+            pairs += len(ids) == 2 and br == {"b0", "b1"}
+    assert pairs >= 10, pairs
+    # the last per-slice level is lane-merged and read only by the output permute: its lanes are
+    # summed before one permute per batch (Op::lane_sum on a sweep2 level)
+    assert any(l.startswith("[slice]") and "SWEEP2" in l and "lane-sum" in l for l in ops)
