@@ -398,13 +398,27 @@ def main():
     t_plan0 = time.perf_counter()
     base = config_task(args.config)
     bitstrings = args.shard == "bitstrings"
-    # bitstring sharding: rank r's amplitude block r (same network and plan, other fixed bits)
-    task = with_batch(base, args.batch + (rank if bitstrings else 0)) if (bitstrings or args.batch) else base
-    expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
-    ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
+    inflight = max(1, args.inflight) if bitstrings else 1
+    pipe = None
+    if bitstrings:
+        # bitstring sharding (sampling.BlockPipeline): rank r contracts blocks batch + r + N k, k =
+        # 0, 1, ... (a window of 64 distinct blocks, cycled) -- the same network and plan with other
+        # fixed bits, one projector-table copy per step -- on `inflight` plans with their own
+        # arenas and streams; step k runs on plan k mod inflight
+        from tneq_qc_amd.sampling import BlockPipeline
+        pipe = BlockPipeline(base, [args.batch + rank + world * k for k in range(max(64, inflight))],
+                             inflight=inflight, device=dev)
+        task = with_batch(base, args.batch + rank)
+        expr, ops, out = pipe.slots[0][0], pipe.slots[0][1], pipe.slots[0][3]
+        pipe.step()   # slot 0's projector buffer holds block batch + r (the latency / profiled passes)
+        pipe.k = 0
+    else:
+        task = with_batch(base, args.batch) if args.batch else base
+        expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
+        ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
+        out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
     plan = expr.plan(torch.complex64)
     n_slices = plan.n_slices
-    out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
     t_plan = time.perf_counter() - t_plan0
 
     def slices_job():
@@ -439,28 +453,17 @@ def main():
         """One block on the current stream (plan 0): the latency pass and the profiled passes."""
         expr(*ops, out=out)
 
-    inflight = max(1, args.inflight) if bitstrings else 1
     if bitstrings:
-        # every rank contracts all slices of its own blocks: no collective on the data path.  Slot i
-        # of rank r holds block batch + r + N*i (its own plan, arena, operands and stream); step k
-        # runs on slot k % inflight, so up to `inflight` blocks are in flight on the GPU
-        slots = [(expr, ops, out, torch.cuda.current_stream(dev))]
-        for i in range(1, inflight):
-            ti = with_batch(base, args.batch + rank + world * i)
-            ei = HipContractExpression(ti.eq, *ti.shapes, optimize=ti.path, slices=ti.sliced)
-            slots.append((ei, [torch.from_numpy(o).to(dev, torch.complex64) for o in ti.operands],
-                          torch.empty(ei.out_shape, dtype=torch.complex64, device=dev), torch.cuda.Stream(dev)))
-        nstep = [0]
-
         def step():
-            e_i, ops_i, out_i, s_i = slots[nstep[0] % inflight]
-            with torch.cuda.stream(s_i):
-                e_i(*ops_i, out=out_i)
-            nstep[0] += 1
+            pipe.step()
 
         def last_out():
-            torch.cuda.synchronize()
-            return out
+            # block batch + r again on slot 0 (the saved block is deterministic per rank)
+            pipe.synchronize()
+            pipe.k = 0
+            o = pipe.step()
+            pipe.synchronize()
+            return o
     else:
         step, last_out = slices_job()
 
