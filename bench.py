@@ -9,9 +9,11 @@ config C4 of SURVEY.md §8(d): a 53-qubit depth-20 brick-wall random circuit (52
 boundary MFMA GEMM, the sweeps' deferred tails per slice (slice-invariant work hoisted).
 
 Ranks (`--shard`):
-* bitstrings (default): rank r contracts amplitude block r -- the same network with the closed
-  qubits' fixed bits flipped by r's binary digits (circuits.with_batch), so one compiled plan --
-  over all its slices, with no collective on the data path: per-GPU work is fixed as N grows
+* bitstrings (default): rank r contracts amplitude blocks r, r + N, r + 2N, ... (a different block
+  every step, a window of 64 cycled) -- the same network with the closed qubits' fixed bits
+  flipped by the block index's binary digits (circuits.with_batch), so one compiled plan -- over
+  all its slices, two blocks in flight on their own plans and streams (sampling.BlockPipeline),
+  with no collective on the data path: per-GPU work is fixed as N grows
   ("scaling": "weak"; value = N blocks x 2^20 amplitudes / max-over-ranks time).  The same ranks
   then time ONE block with its slices sharded over them + one RCCL all-reduce (SUM) of the
   partial amplitudes over xGMI (`slices_strong`, the reference's sliced path,
