@@ -6,7 +6,7 @@ only the closed qubits' projector operands change (circuits.with_batch), so one 
 serves every block.  `BlockPipeline` keeps `inflight` plans (each with its own arena, operands,
 output and HIP stream) and runs block k on plan k mod inflight: the sweeps of one block are
 latency-bound, and a second block's launches fill the idle compute units
-(C4: 0.75 -> 0.49 ms per block with two in flight).
+(C4: 0.69 ms per block one at a time, 0.47 / 0.41 with two / four in flight).
 
 Block b's projector vectors come from a device table built once per pipeline (`blocks` given up
 front); a step copies its row into the plan's projector buffer on the plan's stream (one small
