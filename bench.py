@@ -12,7 +12,8 @@ Ranks (`--shard`):
 * bitstrings (default): rank r contracts amplitude blocks r, r + N, r + 2N, ... (a different block
   every step, a window of 64 cycled) -- the same network with the closed qubits' fixed bits
   flipped by the block index's binary digits (circuits.with_batch), so one compiled plan -- over
-  all its slices, two blocks in flight on their own plans and streams (sampling.BlockPipeline),
+  all its slices, four blocks in flight (`--inflight`) on their own plans and streams
+  (sampling.BlockPipeline),
   with no collective on the data path: per-GPU work is fixed as N grows
   ("scaling": "weak"; value = N blocks x 2^20 amplitudes / max-over-ranks time).  The same ranks
   then time ONE block with its slices sharded over them + one RCCL all-reduce (SUM) of the
@@ -24,14 +25,17 @@ Inputs (cores, vectors) are resident in HBM before timing.
 C2 = one amplitude, no slicing; C4g / C3d: other paths of the C4 / C3 networks).
 
 Timing: the headline (`value`, `ms_per_step`) is the production launch path — every step replays
-the plan's captured hipGraph, no events inside (two blocks in flight, see above).  The dominant
+the plan's captured hipGraph, no events inside (several blocks in flight, see above).  The dominant
 kernel's duration (`roofline`) is then measured in separate single-stream passes of the same steps
 in which the plan launches eagerly with HIP events around every launch of that kernel kind on its
 stream (the kernels are identical); rocprofv3's average for the same command, committed under
 profiles/, is reported beside it (`*_rocprof`).
 
-Prints ONE JSON line on rank 0 with `roofline` and, at N=1, `cpu_baseline` (the oracle's numpy
-pairwise executor on a bounded sample of the same network, in the same dtype).
+Output: the LAST stdout line on rank 0 is ONE compact JSON headline (<= 2 KB, `headline_line`)
+with `roofline` and, at N=1, `cpu_baseline` (the oracle's numpy pairwise executor on a bounded
+sample of the same network, in the same dtype) and one [value, ms, frac] triple per secondary
+line; the secondary sections in full go to stderr (`[bench-detail]` lines) and, with `--details
+PATH`, to a JSON file.
 
 Ranks: under torch.distributed.run (WORLD_SIZE set) every process is one rank on cuda:LOCAL_RANK.
 `--gpus N` without WORLD_SIZE launches the N ranks itself (the env launch of the reference,
@@ -281,6 +285,25 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
     return out
 
 
+def _child_details(cmd, env=None) -> dict:
+    """Run a child bench.py (no exec) and return its full result (its --details file)."""
+    import subprocess
+    import tempfile
+    fd, path = tempfile.mkstemp(suffix=".json", prefix="bench_child_")
+    os.close(fd)
+    try:
+        r = subprocess.run(cmd + ["--details", path], env=env, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(f"child bench rc {r.returncode}: {r.stderr[-400:]}")
+        with open(path) as f:
+            return json.load(f)
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+
+
 def alt_gemm(args, envs: dict, desc: str, cfg: str):
     """Config `cfg` with another complex64 boundary-GEMM kernel (library switches in `envs`,
     read once per process: a child process, started without exec)."""
@@ -288,9 +311,7 @@ def alt_gemm(args, envs: dict, desc: str, cfg: str):
     env = dict(os.environ, **envs)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-c5", "--no-alt", "--no-other"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
-    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
-    d = json.loads(line)
+    d = _child_details(cmd, env)
     return {"config": cfg, "value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
             "gemm": f"{desc} ({' '.join(f'{k}={v}' for k, v in envs.items())})", "roofline": d["roofline"]}
 
@@ -305,9 +326,7 @@ def other_config(args, cfg: str):
            "--cpu-seconds", str(args.other_cpu_seconds)]
     if args.no_cpu_baseline:
         cmd.append("--no-cpu-baseline")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
-    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
-    d = json.loads(line)
+    d = _child_details(cmd)
     return {k: d[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "hbm_kernels", "cpu_baseline",
                               "plan") if k in d}
 
@@ -367,6 +386,9 @@ def main():
                     help="skip the C2 / C3 secondary lines (child processes, N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (seconds of oracle work at every host core)")
+    ap.add_argument("--details", default=None,
+                    help="write the full result (every secondary section) to this JSON file; stdout's "
+                         "last line is the compact headline either way")
     ap.add_argument("--other-cpu-seconds", type=float, default=4.0,
                     help="CPU-baseline budget of the C2 / C3 secondary lines")
     args = ap.parse_args()
@@ -791,9 +813,123 @@ def main():
         except Exception as e:  # the secondary line must never hide the headline
             res["c5_train"] = {"error": repr(e)}
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res, args.details or os.environ.get("TQ_BENCH_DETAILS"))
     if world > 1:
         dist.destroy_process_group()
+
+
+# ---- output: the driver parses the LAST stdout line (its tail holds a few KB), so that line is
+# the compact headline; every secondary section goes to stderr as one `[bench-detail]` line each
+# and, with --details / TQ_BENCH_DETAILS, the full result to a JSON file
+HEADLINE_MAX_BYTES = 2048   # well inside the driver's stdout tail
+SECONDARY_KEYS = ("config_C2", "config_C3", "config_C4g", "config_C4x4", "config_C3d", "c5_train",
+                  "alt_f16_gemm_side_split", "alt_bf16_split", "alt_f32_mfma")
+
+
+def _short(s, n: int):
+    s = "" if s is None else str(s)
+    return s if len(s) <= n else s[: n - 3] + "..."
+
+
+def _sig(x, n: int = 5):
+    """A float rounded to n significant digits (the compact line's secondary numbers)."""
+    if not isinstance(x, float) or x == 0.0 or x != x:
+        return x
+    return float(f"{x:.{n}g}")
+
+
+def _pick(d, keys):
+    d = d or {}
+    return {k: d[k] for k in keys if k in d}
+
+
+def headline(res: dict) -> dict:
+    """The compact headline object (the last stdout line): the contract keys, the dominant
+    kernel's roofline, the CPU baseline and one [value, ms, frac] triple per secondary line."""
+    h = _pick(res, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                    "scaling", "vs_baseline", "dtype", "data"))
+    cfg = dict(res.get("config") or {})
+    if "workload" in cfg:
+        cfg["workload"] = _short(cfg["workload"], 160)
+    h["config"] = _rounded(cfg)
+    t = res.get("timing") or {}
+    h["timing"] = _rounded(_pick(t, ("inflight", "group", "latency_ms_per_step", "eager_profiled_ms_per_step")))
+    rf = res.get("roofline") or {}
+    r = _rounded(_pick(rf, ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_vs_algorithmic",
+                            "frac_rocprof", "avg_launch_us_events", "avg_launch_us_rocprof", "launches_timed",
+                            "algorithmic_bytes_per_step", "aggregate_GBps", "aggregate_frac",
+                            "clock_GHz_in_kernel")))
+    r["kernel"] = _short(rf.get("kernel"), 60)
+    for k in ("traffic_source", "rocprof_source"):
+        if k in rf:
+            r[k] = _short(rf[k], 60)
+    h["roofline"] = r
+    if res.get("roofline_gemm"):
+        h["roofline_gemm"] = _rounded(_pick(res["roofline_gemm"], ("achieved", "peak", "unit", "frac")))
+    cb = res.get("cpu_baseline")
+    if cb:
+        h["cpu_baseline"] = _rounded(_pick(cb, ("value", "unit", "cores", "kind", "cpu_model", "error")))
+        if "sample" in cb:
+            h["cpu_baseline"]["sample"] = _short(cb["sample"], 100)
+    sec = {}
+    for k in SECONDARY_KEYS:
+        v = res.get(k)
+        if not v:
+            continue
+        # [value, ms per step, roofline frac] (units: the section's, in the --details file)
+        e = [_sig(v.get("value")), _sig(v.get("ms_per_step")),
+             _sig((v.get("roofline") or {}).get("frac") if isinstance(v.get("roofline"), dict) else None)]
+        if "error" in v:
+            e = {"error": _short(v["error"], 60)}
+        sec[k.replace("config_", "").replace("alt_", "")] = e
+    p = res.get("permute")
+    if p:
+        sec["permute"] = [_sig(p.get("GBps")), _sig(p.get("frac")), p.get("bit_exact")]
+    if res.get("slices_strong"):
+        ss = res["slices_strong"]
+        sec["slices_strong"] = [_sig(ss.get("value")), _sig(ss.get("ms_per_step")), ss.get("parallelism")]
+    if sec:
+        h["secondary"] = sec
+    return h
+
+
+def _rounded(d: dict) -> dict:
+    return {k: _sig(v) for k, v in d.items()}
+
+
+def headline_line(res: dict) -> str:
+    """`headline(res)` as one JSON line of at most HEADLINE_MAX_BYTES (secondary numbers, then
+    long strings dropped if it would not fit)."""
+    h = headline(res)
+    s = json.dumps(h, separators=(",", ":"))
+    if len(s) > HEADLINE_MAX_BYTES:
+        h.pop("secondary", None)
+        s = json.dumps(h, separators=(",", ":"))
+    if len(s) > HEADLINE_MAX_BYTES:
+        for sect in (h, h.get("roofline", {}), h.get("timing", {}), h.get("cpu_baseline", {}), h.get("config", {})):
+            for k, v in list(sect.items()):
+                if isinstance(v, str) and len(v) > 60 and k not in ("metric", "unit"):
+                    sect[k] = _short(v, 60)
+        s = json.dumps(h, separators=(",", ":"))
+    return s
+
+
+def emit(res: dict, details_path=None) -> None:
+    """Secondary sections -> stderr (one line each), full result -> `details_path` (optional),
+    the compact headline -> the last stdout line."""
+    for k, v in res.items():
+        if isinstance(v, dict) and k not in ("config", "timing"):
+            print(f"[bench-detail] {k} {json.dumps(v, separators=(',', ':'))}", file=sys.stderr, flush=True)
+    if details_path:
+        try:
+            d = os.path.dirname(os.path.abspath(details_path))
+            os.makedirs(d, exist_ok=True)
+            with open(details_path, "w") as f:
+                json.dump(res, f, indent=1)
+        except OSError as e:
+            print(f"[bench] could not write {details_path}: {e!r}", file=sys.stderr, flush=True)
+    sys.stderr.flush()
+    print(headline_line(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -105,6 +105,16 @@ int tq_gemm_batched(int dtype, int transA, int transB, int64_t M, int64_t N, int
                     int64_t strideC, void* workspace, size_t ws_bytes, void* stream);
 size_t tq_gemm_workspace_size(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch);
 
+/* The pre-split ("planes") boundary GEMM of a plan (tq_gemmp.hip; the C4g path): the f32 split-K
+ * partials a launch of up to `batch` lane entries needs (the max over every batch size <= batch:
+ * a partial lane batch may choose more K splits), and the launcher's argument checks without a
+ * launch (TQ_OK, or TQ_ERR_INVALID when the shape is unsupported or the partials exceed
+ * ws_bytes).  Host-only: CPU tests of the sizing.  Replaces nothing in the reference (a
+ * workspace of this engine's GEMM behind einsum_strategy.py:622-643's tensordot). */
+size_t tq_planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch);
+int tq_planes_gemm_check(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t lda, int64_t ldb,
+                         size_t ws_bytes);
+
 /* y = x + beta * y over n elements (used to sum partial amplitudes of slices) */
 int tq_axpy(int dtype, int64_t n, const void* x, void* y, double beta, void* stream);
 

@@ -21,7 +21,7 @@ TQ_OK, TQ_ERR_INVALID, TQ_ERR_HIP, TQ_ERR_ALLOC, TQ_ERR_UNSUPPORTED = 0, -1, -2,
 EXPORTED = (
     "tq_version", "tq_last_error", "tq_device_synchronize", "tq_library_query", "tq_library_set", "tq_permute",
     "tq_gemm_batched",
-    "tq_gemm_workspace_size", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
+    "tq_gemm_workspace_size", "tq_planes_gemm_workspace", "tq_planes_gemm_check", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
     "tq_plan_create", "tq_plan_query", "tq_plan_set", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
     "tq_plan_profile", "tq_plan_profile_read", "tq_hermite_features", "tq_inverse_cdf_sample",
     "tq_sgdg_step", "tq_fidelity_forward", "tq_fidelity_backward",
@@ -55,6 +55,9 @@ _SIGS = {
                                    _c.c_int64, _c.c_double, _vp, _c.c_int64, _c.c_int64, _vp,
                                    _c.c_size_t, _vp]),
     "tq_gemm_workspace_size": (_c.c_size_t, [_c.c_int, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64]),
+    "tq_planes_gemm_workspace": (_c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64]),
+    "tq_planes_gemm_check": (_c.c_int, [_c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64,
+                                        _c.c_size_t]),
     "tq_axpy": (_c.c_int, [_c.c_int, _c.c_int64, _vp, _vp, _c.c_double, _vp]),
     "tq_contract_pair_workspace": (_c.c_size_t, [_c.c_int, _c.c_int, _i64p, _i32p, _c.c_int, _i64p,
                                                  _i32p, _c.c_int, _i32p]),

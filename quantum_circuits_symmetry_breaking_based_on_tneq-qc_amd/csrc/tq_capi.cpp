@@ -142,6 +142,18 @@ int tq_gemm_batched(int dtype, int transA, int transB, int64_t M, int64_t N, int
   TQ_GUARD_END
 }
 
+size_t tq_planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (M < 1 || N < 1 || K < 1 || batch < 1) return 0;
+  return tq::planes_gemm_workspace(M, N, K, batch);
+}
+
+int tq_planes_gemm_check(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t lda, int64_t ldb,
+                         size_t ws_bytes) {
+  TQ_GUARD_BEGIN
+  return tq::planes_gemm_check(M, N, K, batch, lda, ldb, ws_bytes);
+  TQ_GUARD_END
+}
+
 size_t tq_gemm_workspace_size(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch) {
   if (!tq::dtype_valid(dtype)) return 0;
   return tq::gemm_workspace(dtype, M, N, K, batch);
@@ -307,6 +319,16 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "planes_gemm") return P.planes_gemm >= 0 ? 1 : 0;   // a pre-split boundary GEMM was planned
   if (k == "planes_active") return (P.planes_gemm >= 0 && P.use_planes && (P.d_planes || !P.d_arena)) ? 1 : 0;
   if (k == "planes_bytes") return (int64_t)P.planes_bytes;
+  // the planes GEMM's shape and partials workspace (host-side layout: no GPU needed)
+  if (k == "planes_ws_bytes") return P.planes_gemm >= 0 ? (int64_t)(P.planes_sc_off - P.planes_ws_off) : 0;
+  if (P.planes_gemm >= 0 && k.rfind("planes_gemm_", 0) == 0) {
+    const tq::Op& g = P.ops[P.planes_gemm];
+    if (k == "planes_gemm_M") return g.M;
+    if (k == "planes_gemm_N") return g.N;
+    if (k == "planes_gemm_K") return g.K;
+    if (k == "planes_gemm_lda") return g.lda;
+    if (k == "planes_gemm_ldb") return g.ldb;
+  }
   if (k == "out_numel") return P.out_numel;
   return -1;
 }

@@ -252,17 +252,23 @@ size_t planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch) {
   return w;
 }
 
-int planes_gemm_launch(const PlanesGemmArgs& a0, const PlanesCombineArgs& c0, hipStream_t stream) {
-  if (!planes_gemm_ok(a0.M, a0.N, a0.K, a0.lda, a0.ldb) || a0.batch < 1) {
+// the launcher's argument checks, host only (tq_planes_gemm_check: CPU tests of the sizing)
+int planes_gemm_check(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t lda, int64_t ldb, size_t ws_bytes) {
+  if (!planes_gemm_ok(M, N, K, lda, ldb) || batch < 1) {
     set_error("planes gemm: unsupported shape");
     return TQ_ERR_INVALID;
   }
-  PlanesGemmArgs a = a0;
-  a.splits = planes_gemm_splits(a.M, a.N, a.K, a.batch);
-  if (planes_ws_one(a.M, a.N, a.K, a.batch) > a.ws_bytes) {
+  if (planes_ws_one(M, N, K, batch) > ws_bytes) {
     set_error("planes gemm: partials exceed the workspace");
     return TQ_ERR_INVALID;
   }
+  return TQ_OK;
+}
+
+int planes_gemm_launch(const PlanesGemmArgs& a0, const PlanesCombineArgs& c0, hipStream_t stream) {
+  TQ_TRY(planes_gemm_check(a0.M, a0.N, a0.K, a0.batch, a0.lda, a0.ldb, a0.ws_bytes));
+  PlanesGemmArgs a = a0;
+  a.splits = planes_gemm_splits(a.M, a.N, a.K, a.batch);
   const int64_t nwg = (int64_t)a.batch * 3 * a.splits * (a.M / kBM) * (a.N / kBN);
   hipLaunchKernelGGL(gemm_planes_kernel, dim3((unsigned)nwg), dim3(kNT), 0, stream, a);
   TQ_HIP(hipGetLastError());

@@ -1921,7 +1921,8 @@ class Compiler {
       }
       // Barriers between passes (kS2PmSync, bit 16 of a pass's count word: the workgroup barrier
       // before that pass).  Thread t of the 512 takes the groups gi = t (mod 512) in every pass
-      // (tq_sweep2.hip gate_pass_u / block_pass), so wave w owns the groups whose gi bits 6..8 are
+      // (tq_sweep2.hip gate_pass_u / block_pass), so wave w owns the groups whose gi bits 6..8
+      // (kS2WaveBits .. kS2LogThreads - 1, asserted in the kernel) are
       // w, i.e. the elements whose address bits behind those group bits (columns below logC, then
       // the pass positions in ascending order) are w.  Two consecutive passes with the same
       // wave-select address bits leave every element with one wave: no barrier between them (LDS
@@ -1930,7 +1931,7 @@ class Compiler {
         const uint32_t mask = (uint32_t)d.k.pmeta[q][kS2PmPass];
         const int lg = d.logC + __builtin_popcount(mask);   // log2 groups
         std::vector<int> sig;
-        for (int b = 6; b <= 8 && b < lg; ++b) {
+        for (int b = kS2WaveBits; b < kS2LogThreads && b < lg; ++b) {
           if (b < d.logC) { sig.push_back(-1 - b); continue; }
           uint32_t m = mask;
           for (int t = 0; t < b - d.logC; ++t) m &= m - 1;
@@ -2551,7 +2552,20 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
                path, n_sliced, sliced_modes) == TQ_OK && Q.lanes == P.lanes)
       P = std::move(Q);
   }
+  plan_planes_layout(P);   // sizes known at compile time (queries, CPU tests); allocated at materialize
   return TQ_OK;
+}
+
+void plan_planes_layout(Plan& P) {
+  if (P.planes_gemm < 0) return;
+  const Op& g = P.ops[P.planes_gemm];
+  const size_t lanes = (size_t)std::max(1, P.lanes);
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  P.planes_lane_bytes = al((size_t)12 * (size_t)(P.planes_n[0] + P.planes_n[1]));
+  P.planes_ws_off = lanes * P.planes_lane_bytes;
+  // every lane-batch size up to the lane count: a partial batch may pick more K splits (r05c)
+  P.planes_sc_off = P.planes_ws_off + al(planes_gemm_workspace(g.M, g.N, g.K, (int64_t)lanes));
+  P.planes_bytes = P.planes_sc_off + al(lanes * 2 * sizeof(int32_t));
 }
 
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
@@ -2579,13 +2593,7 @@ int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
   if (P.n_ps && !P.h_bad) TQ_HIP(hipHostMalloc((void**)&P.h_bad, P.n_slices * sizeof(uint32_t), hipHostMallocDefault));
   // the pre-split boundary GEMM's planes, partials and scale words (plan-owned plans only)
   if (P.planes_gemm >= 0 && P.owns_device && !P.d_planes) {
-    const Op& g = P.ops[P.planes_gemm];
-    const size_t lanes = (size_t)std::max(1, P.lanes);
-    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-    P.planes_lane_bytes = al((size_t)12 * (size_t)(P.planes_n[0] + P.planes_n[1]));
-    P.planes_ws_off = lanes * P.planes_lane_bytes;
-    P.planes_sc_off = P.planes_ws_off + al(planes_gemm_workspace(g.M, g.N, g.K, (int64_t)lanes));
-    P.planes_bytes = P.planes_sc_off + al(lanes * 2 * sizeof(int32_t));
+    plan_planes_layout(P);
     if (hipMalloc(&P.d_planes, P.planes_bytes) != hipSuccess) {
       (void)hipGetLastError();
       P.d_planes = nullptr;   // no room: the GEMM-side split path runs instead

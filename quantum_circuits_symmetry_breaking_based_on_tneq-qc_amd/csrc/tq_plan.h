@@ -233,6 +233,8 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
                  const int64_t* in_extents, const int64_t* in_strides, int out_rank,
                  const int32_t* out_modes, int n_steps, const int32_t* path, int n_sliced,
                  const int32_t* sliced_modes);
+// the pre-split boundary GEMM's buffer layout (planes, partials, scale words): host only
+void plan_planes_layout(Plan& P);
 // upload tables / allocate arena (owned) — or use caller memory when `arena`/`tables` are given
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream);
 int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,

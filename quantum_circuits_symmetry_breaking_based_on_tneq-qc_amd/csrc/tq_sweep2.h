@@ -27,6 +27,10 @@ constexpr int kS2ChunkBytes = 65536;   // LDS tile per workgroup
 constexpr int kS2MaxChunkBits = 13;    // log2(chunk elements) for 8-byte elements
 constexpr int kS2MaxColBits = 48;
 constexpr int kS2LogThreads = 9;       // 512 threads per workgroup
+// Pass barriers (kS2PmSync, planned in tq_plan.cpp s2_layout): thread t takes the groups
+// gi == t (mod 2^kS2LogThreads) of every pass, so the 64-lane wave w owns exactly the groups whose
+// gi bits [kS2WaveBits, kS2LogThreads) equal w.  The kernel asserts both constants.
+constexpr int kS2WaveBits = 6;         // log2(wave size): CDNA waves are 64 lanes
 constexpr int kS2MaxSlots = 16;        // chunk elements per thread (load / store register slots)
 constexpr int kS2MaxPos = 10;         // tile positions (index bits), at most
 inline int s2_max_pos(int esz) { return esz > 8 ? 9 : 10; }

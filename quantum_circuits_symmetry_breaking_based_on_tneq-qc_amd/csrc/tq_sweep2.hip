@@ -38,6 +38,10 @@ namespace tq {
 namespace {
 
 constexpr int NT = 512, LOG_NT = 9;
+// the pass-barrier elision (kS2PmSync) assumes gi == threadIdx.x (mod NT) in gate_pass_u and
+// block_pass and 64-lane waves: wave = gi bits [kS2WaveBits, kS2LogThreads)
+static_assert(NT == (1 << kS2LogThreads) && LOG_NT == kS2LogThreads, "sweep2 thread count vs the planner's");
+static_assert(kS2WaveBits == 6 && kS2LogThreads > kS2WaveBits, "wave-select group bits");
 constexpr int kLut = 64;                     // per-gate group tables: 32 entries for the low 5 pass bits,
                                              // 32 for the high ones (<= 9 pass positions)
 constexpr int kCf = kS2MaxK * kS2MaxKN;      // coefficient slots per gate
@@ -468,6 +472,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   const int32_t* const pmeta = &keep.pmeta[0][0];        // passes
   const int32_t* const lut = &keep.lut[0][0];            // group -> LDS byte offset part
   const int tid = threadIdx.x;
+  if (__builtin_amdgcn_wavefrontsize() != (1 << kS2WaveBits)) __builtin_trap();   // folded: wave64
   // ---- which op this workgroup works on: one op of a level (blockIdx ranges select it,
   // wave-uniform scan), or -- S2Launch::seq, one workgroup -- every op of a dependent chain in
   // order: op j + 1 reads what op j stored (same CU: its stores are complete before the next

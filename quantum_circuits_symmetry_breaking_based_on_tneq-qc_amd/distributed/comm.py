@@ -431,6 +431,11 @@ def get_comm_backend(backend: Union[str, CommBackendType] = "torch", **kwargs) -
             return CommTorch(**{k: v for k, v in kwargs.items() if k in (
                 "torch_backend", "init_method", "world_size", "rank", "node_rank", "num_nodes", "auto_init", "group")})
         except Exception as e:  # the reference's fallback (comm_factory.py:152-156)
+            ws = kwargs.get("world_size") or int(os.environ.get("WORLD_SIZE", "1"))
+            if ws > 1:
+                # a multi-rank launch whose process group failed must not continue as a mock:
+                # its collectives would silently be no-ops
+                raise RuntimeError(f"torch.distributed could not be initialised for world size {ws}: {e}") from e
             print(f"Warning: PyTorch distributed not available ({e}), falling back to MockCommTorch")
             return MockCommTorch(kwargs.get("rank"), kwargs.get("world_size"), kwargs.get("node_rank"),
                                  kwargs.get("num_nodes"))
@@ -469,8 +474,15 @@ def comm_group(comm):
 
 
 def comm_rank_size(comm) -> Tuple[int, int]:
-    """(rank, world size) of `comm`: the CommBase's own numbers (a mock reports its configured
-    ones), else the process group's (1 rank without an initialised group)."""
+    """(rank, world size) of `comm`: the CommBase's own numbers, else the process group's (1 rank
+    without an initialised group).  A mock runs no collectives (`comm_group` is WORLD), so a mock
+    configured with world_size > 1 is refused here rather than set up as partitions whose
+    exchanges would reach torch.distributed with no process group."""
+    if isinstance(comm, MockCommTorch):
+        if comm.world_size > 1:
+            raise ValueError(f"MockCommTorch(world_size={comm.world_size}) runs no collectives; a multi-rank "
+                             "engine needs a torch process group (CommTorch / get_comm_backend('torch'))")
+        return 0, 1
     if isinstance(comm, CommBase):
         return comm.rank, comm.world_size
     if dist.is_available() and dist.is_initialized():

@@ -89,11 +89,18 @@ class TreeContraction:
 
     Gradients: every rank must run its backward (the stage adjoints are collectives); a rank
     whose partition is empty differentiates w.r.t. `self.leaf` (its scalar 1), since
-    torch.autograd.grad only runs the nodes on a path to the requested inputs."""
+    torch.autograd.grad only runs the nodes on a path to the requested inputs.
+
+    `scaled`: whether log-scales travel with the stage blocks (TNTensor operands).  Every rank of
+    the group must agree -- a rank sees only its own partition's operands -- so it is either
+    given here or agreed on the first call by one all-reduce (MAX) of the ranks' "I hold a
+    TNTensor" flags, then fixed: a later call with TNTensor operands on an unscaled contraction
+    raises instead of posting messages the other ranks would never match."""
 
     def __init__(self, eq: str, shapes: Sequence[Sequence[int]], group=None,
                  partitions: Optional[Sequence[Sequence[int]]] = None,
-                 executor: Optional[Callable] = None, optimize="greedy"):
+                 executor: Optional[Callable] = None, optimize="greedy", scaled: Optional[bool] = None):
+        self.scaled = scaled
         self.net = parse_equation(eq, shapes)
         net = self.net
         self.group = group
@@ -185,7 +192,13 @@ class TreeContraction:
         mine = self.parts[r]
         ref = next(o for o in operands if o is not None)
         ref = ref.tensor if isinstance(ref, TNTensor) else ref
-        tn = any(isinstance(o, TNTensor) for o in operands if o is not None)
+        tn_here = any(isinstance(o, TNTensor) for o in operands if o is not None)
+        if self.scaled is None:
+            self.scaled = _agree_any(tn_here, ref, self.group) if self.world > 1 else tn_here
+        elif tn_here and not self.scaled:
+            raise ValueError("TreeContraction: TNTensor operands on a contraction agreed unscaled (its first "
+                             "call had none on any rank); construct it with scaled=True")
+        tn = self.scaled
         raw, log_scale, sign = [], 0.0, 1.0
         for t in mine:
             o = operands[t]
@@ -288,6 +301,14 @@ def _staged(t: torch.Tensor, group) -> bool:
     """gloo moves host memory only: device tensors go through a host copy there (RCCL takes
     them directly)."""
     return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _agree_any(flag: bool, ref: torch.Tensor, group) -> bool:
+    """True on every rank of `group` when `flag` is True on any (one all-reduce MAX)."""
+    on_dev = ref.is_cuda and dist.get_backend(group) != "gloo"
+    t = torch.tensor([1.0 if flag else 0.0], device=ref.device if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item() > 0)
 
 
 def _first_use(ref: torch.Tensor, group):

@@ -119,8 +119,15 @@ class NativePlan:
         self._h = None
 
     def __del__(self):
+        # a finalizer may run while ANOTHER thread holds a global-mode capture (which a destroy's
+        # hipEventSynchronize / hipGraphExecDestroy / hipFree would invalidate, and the current
+        # stream's capture state does not show): the handle is always parked and released at the
+        # next drain point (plan creation / execution, the end of our own captures) -- ADVICE r5
         try:
-            self.release_now()
+            h = getattr(self, "_h", None)
+            if h is not None and _lib._lib is not None:
+                graphs.defer_release(_PlanHandle(h))
+            self._h = None
         except Exception:  # interpreter shutdown: modules may already be gone
             pass
 
@@ -545,11 +552,11 @@ class _TreeRuntime:
         self.graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
 
     def __del__(self):
-        # dropped inside a caller's capture: HIP would refuse the CUDAGraphs' destruction
-        # (hipGraphExecDestroy), so they are parked until the capture is over (the step plans
-        # park themselves, NativePlan.release_now)
+        # a finalizer may run inside a capture (this thread's or another's): HIP would refuse the
+        # CUDAGraphs' destruction (hipGraphExecDestroy), so they are always parked until the next
+        # drain point (the step plans park themselves, NativePlan.__del__)
         try:
-            if getattr(self, "graphs", None) and graphs.capturing():
+            if getattr(self, "graphs", None):
                 graphs.defer_release(self.graphs)
                 self.graphs = {}
         except Exception:  # interpreter shutdown

@@ -139,3 +139,18 @@ def test_mock_and_factory():
         res = eng.contract_distributed([torch.tensor(s) for s in states], [torch.tensor(x) for x in mx])
         ref = np.abs(greedy_contract(qr, cores, states, mx)) ** 2
         assert np.abs(res.numpy() - ref).max() / np.abs(ref).max() < 1e-12
+    # a mock runs no collectives, so a multi-rank mock is refused up front
+    with pytest.raises(ValueError, match="runs no collectives"):
+        DistributedEngineSiamese(executor=_torch_executor, comm=MockCommTorch(rank=0, world_size=4))
+
+
+def test_failed_multirank_init_does_not_fall_back_to_a_mock(monkeypatch):
+    """A launcher set WORLD_SIZE > 1 but the process group cannot be set up: the factory raises
+    instead of returning a mock whose collectives are no-ops."""
+    from tneq_qc_amd.distributed import get_comm_backend
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29999")
+    with pytest.raises(RuntimeError, match="world size 2"):   # an unknown rendezvous scheme fails at once
+        get_comm_backend("torch", torch_backend="gloo", init_method="nosuchscheme://x", world_size=2, rank=0)

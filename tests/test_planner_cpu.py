@@ -384,3 +384,48 @@ def test_branches_follow_the_boundary_join():
     # the last per-slice level is lane-merged and read only by the output permute: its lanes are
     # summed before one permute per batch (Op::lane_sum on a sweep2 level)
     assert any(l.startswith("[slice]") and "SWEEP2" in l and "lane-sum" in l for l in ops)
+
+
+def _old_planes_ws(M, N, K, lanes):
+    """The r05 sizing before d90d7cb: the partials of a FULL lane batch only."""
+    L = _lib.lib()
+    one = L.tq_planes_gemm_workspace(M, N, K, lanes)   # >= the full batch's own need
+    # the full batch's own need = 3 x batch x splits(batch) x M x N x 4 bytes: recover it as the
+    # smallest workspace the check accepts for `lanes`
+    lo, hi = 0, one
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if L.tq_planes_gemm_check(M, N, K, lanes, M, N, mid) == 0:
+            hi = mid
+        else:
+            lo = mid + 1
+    return lo
+
+
+@pytest.mark.parametrize("cfg", ["C4g"])
+def test_planes_gemm_workspace_covers_every_lane_batch(cfg):
+    """VERDICT r5 item 6 (the r05c GPU fault): the planes GEMM's split-K partials must fit every
+    lane-batch size a slice range can produce (a partial batch may pick MORE splits than a full
+    one), and the launcher refuses a workspace that is too small -- checked on the host, through
+    the same sizing and argument checks the GPU launch runs (tq_planes_gemm_check), no GPU."""
+    L = _lib.lib()
+    e, p = _plan(config_task(cfg))
+    assert p.query("planes_gemm") == 1
+    M, N, K = (p.query(f"planes_gemm_{k}") for k in "MNK")
+    lda, ldb = p.query("planes_gemm_lda"), p.query("planes_gemm_ldb")
+    lanes = p.query("lanes")
+    ws = p.query("planes_ws_bytes")
+    assert lanes >= 2 and ws > 0
+    assert ws >= L.tq_planes_gemm_workspace(M, N, K, lanes)
+    for b in range(1, lanes + 1):
+        assert L.tq_planes_gemm_check(M, N, K, b, lda, ldb, ws) == 0, (b, _lib.last_error())
+    # the pre-fix sizing (the full batch's own partials) is too small for some partial batch
+    old = _old_planes_ws(M, N, K, lanes)
+    assert any(L.tq_planes_gemm_check(M, N, K, b, lda, ldb, old) != 0 for b in range(1, lanes))
+    # the refusal itself: one byte short of a batch's need
+    need = max(L.tq_planes_gemm_workspace(M, N, K, b) for b in range(1, lanes + 1))
+    worst = [b for b in range(1, lanes + 1) if L.tq_planes_gemm_check(M, N, K, b, lda, ldb, need - 1) != 0]
+    assert worst, "some batch size needs the whole workspace"
+    assert "exceed the workspace" in _lib.last_error()
+    # and unsupported shapes are refused before any sizing
+    assert L.tq_planes_gemm_check(M + 1, N, K, 1, lda, ldb, ws) != 0

@@ -307,3 +307,65 @@ def test_tree_gradients_with_an_empty_partition():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     for rank, e_out, e_g in sorted(q.get(timeout=5) for _ in range(4)):
         assert e_out < 1e-12 and e_g < 1e-10, (rank, e_out, e_g)
+
+
+def _mixed_worker(rank, world, port, q):
+    """a rank passes only its own partition (None elsewhere) and only rank 0's
+    partition holds TNTensors.  The ranks must agree that log-scales travel (one all-reduce
+    MAX on first use): otherwise rank 0 posts scale messages nobody matches (deadlock) or a
+    scale is read as payload.  Every rank gets the TNTensor result; a later TNTensor call on a
+    contraction agreed unscaled raises on the rank that has one."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle.contract_ref import contract
+        from tneq_qc_amd.core.tn_tensor import TNTensor
+        from tneq_qc_amd.distributed import TreeContraction
+        eq, shapes, ops = _network()
+        full = contract(eq, *ops)
+        job = TreeContraction(eq, shapes, executor=_oracle_executor)
+        mine = set(job.parts[rank])
+        args = []
+        for i, o in enumerate(ops):
+            if i not in mine:
+                args.append(None)
+            elif 0 in mine:
+                s = 2.0 ** (5 * (i % 3) - 5)
+                args.append(TNTensor(torch.from_numpy(o / s), scale=s))
+            else:
+                args.append(torch.from_numpy(o))
+        res = job(*args)
+        assert job.scaled is True
+        assert isinstance(res, TNTensor)
+        val = res.tensor.numpy() * np.exp(res.log_scale) * np.sign(res.scale)
+        err = float(np.abs(val - full).max() / np.abs(full).max())
+        # a contraction agreed unscaled refuses TNTensor operands (no unmatched messages)
+        plain = TreeContraction(eq, shapes, executor=_oracle_executor)
+        r2 = plain(*[torch.from_numpy(o) if i in mine else None for i, o in enumerate(ops)])
+        assert plain.scaled is False and not isinstance(r2, TNTensor)
+        raised = False
+        if 0 in mine:   # it raises before any message (the other ranks do not call)
+            try:
+                plain(*args)
+            except ValueError:
+                raised = True
+        q.put((rank, err, raised == (0 in mine)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tree_scales_agreed_with_mixed_partitions(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mixed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, err, ok in sorted(q.get(timeout=5) for _ in range(world)):
+        assert err < 1e-12, (rank, err)
+        assert ok, rank
