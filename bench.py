@@ -375,6 +375,10 @@ def main():
                          "on plan k %% M's stream (each step one whole block; the sweeps are latency-"
                          "bound, so other blocks fill the idle CUs: 2 / 3 / 4 in flight 0.468 / 0.416 / 0.411 ms per "
                          "block); 1 = one stream")
+    ap.add_argument("--group", type=int, default=1,
+                    help="bitstring sharding: blocks per lockstep group (blocks as lanes: every sweep level "
+                         "of the group's blocks is one launch, tq_plan_execute_group); a step is still one "
+                         "block, a group is launched when its last block is enqueued")
     ap.add_argument("--batch", type=int, default=0,
                     help="bitstring sharding: rank r contracts block batch + r (tests: a 1-rank run of "
                          "another rank's block)")
@@ -424,25 +428,30 @@ def main():
     base = config_task(args.config)
     bitstrings = args.shard == "bitstrings"
     inflight = max(1, args.inflight) if bitstrings else 1
+    group = max(1, args.group) if bitstrings else 1
     pipe = None
     if bitstrings:
         # bitstring sharding (sampling.BlockPipeline): rank r contracts blocks batch + r + N k, k =
-        # 0, 1, ... (a window of 64 distinct blocks, cycled) -- the same network and plan with other
-        # fixed bits, one projector-table copy per step -- on `inflight` plans with their own
-        # arenas and streams; step k runs on plan k mod inflight
+        # 0, 1, ... (a window of >= 64 distinct blocks, cycled) -- the same network with other
+        # fixed bits -- `group` blocks per lockstep group (one launch per sweep level for all of
+        # them), `inflight` groups on their own streams and plans
         from tneq_qc_amd.sampling import BlockPipeline
-        pipe = BlockPipeline(base, [args.batch + rank + world * k for k in range(max(64, inflight))],
-                             inflight=inflight, device=dev)
+        pipe = BlockPipeline(base, [args.batch + rank + world * k for k in range(max(64, inflight * group))],
+                             inflight=inflight, group=group, device=dev)
         task = with_batch(base, args.batch + rank)
-        expr, ops, out = pipe.slots[0][0], pipe.slots[0][1], pipe.slots[0][3]
-        pipe.step()   # slot 0's projector buffer holds block batch + r (the latency / profiled passes)
-        pipe.k = 0
+        expr, bound0, out = pipe.expr, pipe.slots[0].bound[0], pipe.slots[0].outs[0]
+        ops = list(bound0.tensors)
+        pipe.step()   # slot 0 member 0's projector buffer holds block batch + r (the latency / profiled passes)
+        pipe.reset()
+        pipe.synchronize()
+        plan = bound0.plan
     else:
         task = with_batch(base, args.batch) if args.batch else base
         expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
         ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
         out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
-    plan = expr.plan(torch.complex64)
+        plan = expr.plan(torch.complex64)
+
     n_slices = plan.n_slices
     t_plan = time.perf_counter() - t_plan0
 
@@ -475,8 +484,12 @@ def main():
         return step, last
 
     def step1():
-        """One block on the current stream (plan 0): the latency pass and the profiled passes."""
-        expr(*ops, out=out)
+        """One block on the current stream (slot 0 member 0's plan): the latency pass and the
+        profiled passes."""
+        if bitstrings:
+            bound0.run(out)
+        else:
+            expr(*ops, out=out)
 
     if bitstrings:
         def step():
@@ -485,7 +498,7 @@ def main():
         def last_out():
             # block batch + r again on slot 0 (the saved block is deterministic per rank)
             pipe.synchronize()
-            pipe.k = 0
+            pipe.reset()
             o = pipe.step()
             pipe.synchronize()
             return o
@@ -501,6 +514,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(k):
             fn()
+        if pipe is not None:
+            pipe.flush()   # a partially filled group is launched inside the timed region
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -547,9 +562,9 @@ def main():
                                        if args.dist_backend == "nccl" else "gloo all-reduce (SUM)"}
         _log(f"slices (strong) on one block: {dts / args.steps * 1e3:.2f} ms/step")
 
-    _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step ({inflight} in flight)")
+    _log(f"headline: {dt / args.steps * 1e3:.2f} ms/step ({inflight} groups of {group} in flight)")
     # ---- one block at a time (one stream): the latency of a step
-    dt_lat = max_over_ranks(timed(args.steps, step1)) if inflight > 1 else dt
+    dt_lat = max_over_ranks(timed(args.steps, step1)) if inflight * group > 1 else dt
     # ---- dominant kernel: the same K steps launched eagerly (one stream) with HIP events around
     # every GEMM
     plan.profile(_lib.TQ_OP_GEMM)
@@ -656,11 +671,12 @@ def main():
         },
         "timing": {
             "headline": ("hipGraph replay of the whole plan per step (production path), no events"
-                         + (f"; {inflight} blocks in flight per GPU (step k on plan k mod {inflight}'s stream, "
-                            f"each step one whole block)" if inflight > 1 else "")),
+                         + (f"; {group} blocks per lockstep group (blocks as lanes), {inflight} groups in flight "
+                            f"per GPU on their own streams (each step one whole block)" if inflight * group > 1 else "")),
             "graph_launches_timed": graphs,
             "eager_profiled_ms_per_step": dt_prof / args.steps * 1e3,
             "inflight": inflight,
+            "group": group,
             "latency_ms_per_step": dt_lat / args.steps * 1e3,
             "latency_definition": "the same K steps one block at a time on one stream (no overlap of steps)",
         },

@@ -152,6 +152,10 @@ int tq_plan_create(tq_plan* plan, int dtype, int n_inputs, const int32_t* in_ran
  * TQ_LANE_ARENA_MB), "n_presplit" (pre-split GEMM candidates), "presplit_fallbacks" (slices
  * re-run on the split path so far).  -1 if unknown. */
 int64_t tq_plan_query(tq_plan plan, const char* key);
+/* A copy of a compiled plan (same schedule, no device state: its own arena and tables at its
+ * first execute) -- one per stream / block in flight without compiling the network again. */
+int tq_plan_clone(tq_plan src, tq_plan* out);
+
 /* Plan options: "graph" = 1 (default) replays the execute's launches from a captured hipGraph,
  * 0 launches them eagerly on the stream (use when the caller captures the stream itself);
  * "sweep_chain" = 1 (default, env TQ_S2_SEQ) runs consecutive hoisted levels that are each one
@@ -173,6 +177,18 @@ int tq_plan_describe(tq_plan plan, char* buf, size_t n);
  * (out = sum + (accumulate ? out : 0)).  inputs[i] are device pointers of the FULL inputs.  */
 int tq_plan_execute(tq_plan plan, const void* const* inputs, void* out, int64_t slice_begin,
                     int64_t slice_end, int64_t slice_step, int accumulate, void* stream);
+
+/* Blocks as lanes: run n plans compiled from the SAME network (same equation, shapes, path,
+ * slicing, dtype, strides; distinct plans, e.g. one per amplitude block of a sampler) in lockstep
+ * on one stream, each on its own inputs[k] (n_inputs pointers) into its own outs[k], over the same
+ * slice range.  Every sweep level / chain launch of all members is ONE kernel launch (their op
+ * lists concatenated); the remaining ops run per member.  Results equal n tq_plan_execute calls.
+ * Replaces: n concurrent executions of the reference's ContractExpression
+ * (einsum_strategy.py:622-643) for n bitstring batches (SURVEY.md §8(e) "shard bitstrings").
+ * Refused (TQ_ERR_INVALID): mismatched plans, repeated plans or outputs, cooperative-chain plans. */
+int tq_plan_execute_group(int n, const tq_plan* plans, const void* const* const* inputs, void* const* outs,
+                          int64_t slice_begin, int64_t slice_end, int64_t slice_step, int accumulate,
+                          void* stream);
 /* Releases the plan's graphs, events, streams and device memory.  TQ_ERR_HIP when HIP refuses a
  * release (e.g. hipGraphExecDestroy / hipFree while a stream capture is in progress in this
  * process): the plan stays valid with whatever it still holds, and a later tq_plan_destroy

@@ -22,7 +22,7 @@ EXPORTED = (
     "tq_version", "tq_last_error", "tq_device_synchronize", "tq_library_query", "tq_library_set", "tq_permute",
     "tq_gemm_batched",
     "tq_gemm_workspace_size", "tq_planes_gemm_workspace", "tq_planes_gemm_check", "tq_axpy", "tq_contract_pair_workspace", "tq_contract_pair",
-    "tq_plan_create", "tq_plan_query", "tq_plan_set", "tq_plan_describe", "tq_plan_execute", "tq_plan_destroy",
+    "tq_plan_create", "tq_plan_clone", "tq_plan_query", "tq_plan_set", "tq_plan_describe", "tq_plan_execute", "tq_plan_execute_group", "tq_plan_destroy",
     "tq_plan_profile", "tq_plan_profile_read", "tq_hermite_features", "tq_inverse_cdf_sample",
     "tq_sgdg_step", "tq_fidelity_forward", "tq_fidelity_backward",
 )
@@ -65,11 +65,14 @@ _SIGS = {
                                     _vp, _c.c_int, _i32p, _vp, _vp, _c.c_size_t, _vp]),
     "tq_plan_create": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _i32p, _i32p, _i64p, _i64p,
                                   _c.c_int, _i32p, _c.c_int, _i32p, _c.c_int, _i32p]),
+    "tq_plan_clone": (_c.c_int, [_vp, _c.POINTER(_vp)]),
     "tq_plan_query": (_c.c_int64, [_vp, _c.c_char_p]),
     "tq_plan_set": (_c.c_int, [_vp, _c.c_char_p, _c.c_int64]),
     "tq_plan_describe": (_c.c_int, [_vp, _c.c_char_p, _c.c_size_t]),
     "tq_plan_execute": (_c.c_int, [_vp, _c.POINTER(_vp), _vp, _c.c_int64, _c.c_int64, _c.c_int64,
                                    _c.c_int, _vp]),
+    "tq_plan_execute_group": (_c.c_int, [_c.c_int, _c.POINTER(_vp), _c.POINTER(_c.POINTER(_vp)), _c.POINTER(_vp),
+                                         _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int, _vp]),
     "tq_plan_destroy": (_c.c_int, [_vp]),
     "tq_plan_profile": (_c.c_int, [_vp, _c.c_int]),
     "tq_plan_profile_read": (_c.c_int, [_vp, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64),

@@ -3,6 +3,7 @@
 #include <string>
 #include <exception>
 #include <new>
+#include <vector>
 
 #include "tq_common.h"
 #include "tq_optim.h"
@@ -240,6 +241,17 @@ int tq_plan_create(tq_plan* out, int dtype, int n_inputs, const int32_t* in_rank
   TQ_GUARD_END
 }
 
+int tq_plan_clone(tq_plan src, tq_plan* out) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(src != nullptr && out != nullptr, "null plan");
+  *out = nullptr;
+  auto* h = new tq_plan_s();
+  tq::plan_clone_compiled(src->plan, h->plan);
+  *out = h;
+  return TQ_OK;
+  TQ_GUARD_END
+}
+
 int tq_plan_set(tq_plan p, const char* key, int64_t value) {
   if (!p || !key) {
     tq::set_error("tq_plan_set: null argument");
@@ -356,6 +368,28 @@ int tq_plan_execute(tq_plan p, const void* const* inputs, void* out, int64_t sli
   const int rc = tq::plan_run(p->plan, inputs, out, slice_begin, slice_end, slice_step, accumulate,
                               (hipStream_t)stream);
   trace("executed", p, rc);
+  return rc;
+  TQ_GUARD_END
+}
+
+int tq_plan_execute_group(int n, const tq_plan* plans, const void* const* const* inputs, void* const* outs,
+                          int64_t slice_begin, int64_t slice_end, int64_t slice_step, int accumulate,
+                          void* stream) {
+  TQ_GUARD_BEGIN
+  TQ_CHECK_ARG(n >= 1 && n <= 64 && plans && inputs && outs, "group of 1..64 plans");
+  std::vector<tq::Plan*> ps((size_t)n);
+  for (int k = 0; k < n; ++k) {
+    TQ_CHECK_ARG(plans[k] != nullptr && inputs[k] != nullptr, "null plan / inputs in a group");
+    if (!plans[k]->materialized) {
+      TQ_TRY(tq::plan_materialize(plans[k]->plan, nullptr, nullptr, (hipStream_t)stream));
+      plans[k]->materialized = true;
+    }
+    ps[k] = &plans[k]->plan;
+  }
+  trace("execute_group", plans[0], n);
+  const int rc = tq::plan_run_group(ps.data(), n, inputs, outs, slice_begin, slice_end, slice_step, accumulate,
+                                    (hipStream_t)stream);
+  trace("executed_group", plans[0], rc);
   return rc;
   TQ_GUARD_END
 }

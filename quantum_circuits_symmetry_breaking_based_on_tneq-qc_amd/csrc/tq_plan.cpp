@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -2556,6 +2557,24 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
   return TQ_OK;
 }
 
+void plan_clone_compiled(const Plan& src, Plan& dst) {
+  dst = src;
+  dst.d_arena = dst.d_tables = dst.d_planes = nullptr;
+  dst.owns_device = false;
+  dst.device = -1;
+  dst.serial = 0;
+  dst.h_bad = nullptr;
+  dst.profile = 0;
+  dst.ev_used.clear();
+  dst.ev_free.clear();
+  dst.graphs.clear();
+  dst.graph_clock = 0;
+  dst.cap_stream = nullptr;
+  dst.graph_builds = dst.graph_launches = 0;
+  dst.ps_fallbacks = 0;
+  dst.run_mode = 0;
+}
+
 void plan_planes_layout(Plan& P) {
   if (P.planes_gemm < 0) return;
   const Op& g = P.ops[P.planes_gemm];
@@ -2568,8 +2587,11 @@ void plan_planes_layout(Plan& P) {
   P.planes_bytes = P.planes_sc_off + al(lanes * 2 * sizeof(int32_t));
 }
 
+uint64_t next_plan_serial();
+
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream) {
   TQ_HIP(hipGetDevice(&P.device));
+  P.serial = next_plan_serial();
   if (arena || tables) {
     P.d_arena = arena;
     P.d_tables = tables;
@@ -2842,473 +2864,695 @@ int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, 
   return TQ_OK;
 }
 
-int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
-                 int64_t s_step, int accumulate, hipStream_t stream) {
-  const size_t esz = P.esz;
-  std::vector<int64_t> in_off(P.n_inputs, 0);
-  const int ns = (int)P.sliced.size();
-  bool first = !accumulate;
-  if (s_begin >= s_end) {
-    if (!accumulate && P.out_numel) TQ_HIP(hipMemsetAsync(out, 0, P.out_numel * esz, stream));
-    return TQ_OK;
-  }
-  // Slices run in batches of P.lanes (slice lanes, Plan::lanes): lane j owns its own copy of the
-  // per-slice arena part, the batch's sweep2 levels share launches across lanes, other ops run
-  // lane by lane in lane order (so output accumulation keeps its order)
-  const int64_t nlanes = std::max(1, P.lanes);
+// ---- executor: one plan, or a GROUP of plans compiled from the same network (blocks as lanes).
+// A group executes its plans' schedules in lockstep: every sweep2 level (and dense-sweep level,
+// and chain launch) of all instances is ONE launch whose op list holds every instance's ops --
+// the slice-lane mechanism with an instance index -- so G amplitude blocks in flight cost the
+// launches of one; the other ops (GEMM, permute, lane sum, ...) run per instance.  A group of one
+// plan is exactly the single-plan executor.
+namespace {
+
+struct Inst {
+  Plan* P = nullptr;
+  const void* const* inputs = nullptr;
+  void* out = nullptr;
   std::vector<std::vector<int64_t>> lane_in_off;
   std::vector<int64_t> lane_sl;
-  int cur = 0;   // lane the launches below address
-  for (int64_t s0 = s_begin; s0 < s_end; s0 += s_step * nlanes) {
-    lane_sl.clear();
-    lane_in_off.clear();
-    for (int64_t sl = s0; sl < s_end && (int64_t)lane_sl.size() < nlanes; sl += s_step) {
-      // decode slice id (row-major over sliced modes) -> per-input element offsets
-      std::vector<int64_t> idx(ns);
-      int64_t rem = sl;
-      for (int q = ns - 1; q >= 0; --q) { idx[q] = rem % P.sliced_ext[q]; rem /= P.sliced_ext[q]; }
-      for (int i = 0; i < P.n_inputs; ++i) {
-        int64_t o = 0;
-        for (int q = 0; q < ns; ++q) o += idx[q] * P.inputs[i].slice_stride[q];
-        in_off[i] = o;
-      }
-      lane_sl.push_back(sl);
-      lane_in_off.push_back(in_off);
+  int cur = 0;             // lane the launches address
+  double beta_out = 0.0;   // the first slice of a non-accumulating call overwrites the output
+  bool first = true;
+  bool lanes_summed = false;
+};
+
+class Exec {
+ public:
+  Exec(std::vector<Inst>& insts, hipStream_t stream) : I_(insts), st_(stream), P0_(*insts[0].P) {}
+
+  int run(int64_t s_begin, int64_t s_end, int64_t s_step, int accumulate);
+
+ private:
+  std::vector<Inst>& I_;
+  hipStream_t st_;
+  Plan& P0_;
+  int lane_gemm_ = 1;   // > 1: the GEMM launch below covers that many lanes
+
+  size_t esz() const { return P0_.esz; }
+  char* ptr(const Inst& x, const BufRef& b) const {
+    const Plan& P = *x.P;
+    switch (b.kind) {
+      case BUF_INPUT: return (char*)x.inputs[b.index] + (x.lane_in_off[x.cur][b.index] + b.off) * P.esz;
+      case BUF_ARENA: return (char*)P.d_arena + P.lane_phys + (size_t)x.cur * P.lane_stride + b.off * P.esz;
+      case BUF_PINNED: return (char*)P.d_arena + b.off * P.esz;
+      case BUF_OUTPUT: return (char*)x.out + b.off * P.esz;
+      case BUF_TABLE: return (char*)P.d_tables + b.off;
     }
-    const int64_t sl = lane_sl[0];
-    cur = 0;
-    auto ptr = [&](const BufRef& b) -> char* {
-      switch (b.kind) {
-        case BUF_INPUT: return (char*)inputs[b.index] + (lane_in_off[cur][b.index] + b.off) * esz;
-        case BUF_ARENA: return (char*)P.d_arena + P.lane_phys + (size_t)cur * P.lane_stride + b.off * esz;
-        case BUF_PINNED: return (char*)P.d_arena + b.off * esz;
-        case BUF_OUTPUT: return (char*)out + b.off * esz;
-        case BUF_TABLE: return (char*)P.d_tables + b.off;
+    return nullptr;
+  }
+  static void set_lane(Inst& x, int j) {
+    x.cur = j;
+    x.beta_out = (x.first && x.cur == 0) ? 0.0 : 1.0;
+  }
+  void set_lane_all(int j) {
+    for (auto& x : I_) set_lane(x, j);
+  }
+  static uint32_t* amax_word(const Inst& x, int w) {
+    return reinterpret_cast<uint32_t*>((char*)x.P->d_tables + x.P->amax_off) + w;
+  }
+  // lane j's copy of max word w: per-slice words have one set per lane (the pre-split mode keeps
+  // one shared set: its scales are predicted per batch)
+  static int lane_amax_stride(const Inst& x, int w) {
+    return (w >= x.P->n_amax_once && !x.P->run_mode) ? x.P->n_amax_slice : 0;
+  }
+  static uint32_t* amax_lane(const Inst& x, int w, int j) { return amax_word(x, w + j * lane_amax_stride(x, w)); }
+  // scale word of per-slice max word w; window flag of slice q
+  static int32_t* sc_word(const Inst& x, int w) {
+    return reinterpret_cast<int32_t*>((char*)x.P->d_tables + x.P->sc_off) + (w - x.P->n_amax_once);
+  }
+  static uint32_t* bad_word(const Inst& x, int64_t q) {
+    return reinterpret_cast<uint32_t*>((char*)x.P->d_tables + x.P->bad_off) + q;
+  }
+  // the pre-split boundary GEMM: lane j's planes of operand r (0 = A, 1 = B) and scale words
+  static _Float16* planes_ptr(const Inst& x, int j, int r) {
+    const Plan& P = *x.P;
+    return reinterpret_cast<_Float16*>((char*)P.d_planes + (size_t)j * P.planes_lane_bytes +
+                                       (r ? (size_t)12 * P.planes_n[0] : 0));
+  }
+  static int32_t* planes_sc(const Inst& x, int j, int r) {
+    return reinterpret_cast<int32_t*>((char*)x.P->d_planes + x.P->planes_sc_off) + 2 * j + r;
+  }
+
+  // profiling (HIP events on the stream; the group's first plan holds the records)
+  Plan::Ev ev_begin(int kind) {
+    Plan::Ev ev{};
+    if (P0_.ev_free.empty()) {
+      if (hipEventCreate(&ev.a) != hipSuccess || hipEventCreate(&ev.b) != hipSuccess) ev.kind = -1;
+    } else {
+      ev = P0_.ev_free.back();
+      P0_.ev_free.pop_back();
+    }
+    if (ev.kind == -1) return ev;
+    ev.kind = kind;
+    ev.flops = 0;
+    ev.bytes = 0;
+    return ev;
+  }
+
+  int launch_one(Inst& x, const Op& op);
+  int fill_s2(const Inst& x, S2Op& o, const Op& op, int stab) const;
+  int launch_chain(int b, int e, int coop);
+  int launch(const std::vector<int>& grp);
+};
+
+int Exec::launch_one(Inst& x, const Op& op) {
+  Plan& P = *x.P;
+  const hipStream_t st = st_;
+  const double beta = op.writes_output ? x.beta_out : 0.0;
+  const bool planes_on = planes_active(P);
+  if (planes_on && op.kind == OP_GEMM && &op == &P.ops[P.planes_gemm]) {
+    // lane batch: entries = the batch's lanes (planes and scale words at their lane strides),
+    // the combine sums them into lane 0's result when the plan sums the lanes (Op::lane_sum)
+    const int j0 = lane_gemm_ > 1 ? 0 : x.cur;
+    PlanesGemmArgs a;
+    a.A = planes_ptr(x, j0, 0);
+    a.B = planes_ptr(x, j0, 1);
+    a.sA = a.sB = (int64_t)(P.planes_lane_bytes / 2);
+    a.psA = P.planes_n[0];
+    a.psB = P.planes_n[1];
+    a.lda = op.lda;
+    a.ldb = op.ldb;
+    a.M = (int)op.M;
+    a.N = (int)op.N;
+    a.K = op.K;
+    a.batch = lane_gemm_;
+    a.W = reinterpret_cast<float*>((char*)P.d_planes + P.planes_ws_off);
+    a.ws_bytes = P.planes_sc_off - P.planes_ws_off;
+    PlanesCombineArgs c;
+    c.sc_a = planes_sc(x, j0, 0);
+    c.sc_b = planes_sc(x, j0, 1);
+    c.sc_stride = 2;
+    c.C = ptr(x, op.c);
+    c.ldc = op.ldc;
+    c.sC = (int64_t)(P.lane_stride / P.esz);
+    c.lane_sum = lane_gemm_ > 1 && op.lane_sum;
+    c.beta = (float)beta;
+    return planes_gemm_launch(a, c, st);
+  }
+  switch (op.kind) {
+    case OP_PERMUTE:
+      TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm], ptr(x, op.a),
+                              ptr(x, op.c), beta, st));
+      break;
+    case OP_GEMM: {
+      if (op.skinny) {
+        SkinnyArgs a = op.sk;
+        a.A = ptr(x, op.a);
+        a.B = ptr(x, op.b);
+        a.C = ptr(x, op.c);
+        a.W = op.ws_bytes ? ptr(x, op.ws) : nullptr;
+        a.beta = beta;
+        TQ_TRY(skinny_strided_launch(P.dtype, a, st));
+        break;
       }
-      return nullptr;
-    };
-    // the first slice of a non-accumulating call overwrites the output, the others add
-    double beta_out = (first && cur == 0) ? 0.0 : 1.0;
-    auto set_lane = [&](int j) {
-      cur = j;
-      beta_out = (first && cur == 0) ? 0.0 : 1.0;
-    };
-    auto amax_word = [&](int w) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.amax_off) + w; };
-    // lane j's copy of max word w: per-slice words have one set per lane (the pre-split mode
-    // keeps one shared set: its scales are predicted per batch)
-    auto lane_amax_stride = [&](int w) { return (w >= P.n_amax_once && !P.run_mode) ? P.n_amax_slice : 0; };
-    auto amax_lane = [&](int w, int j) { return amax_word(w + j * lane_amax_stride(w)); };
-    // scale word of per-slice max word w; window flag of slice q
-    auto sc_word = [&](int w) { return reinterpret_cast<int32_t*>((char*)P.d_tables + P.sc_off) + (w - P.n_amax_once); };
-    auto bad_word = [&](int64_t q) { return reinterpret_cast<uint32_t*>((char*)P.d_tables + P.bad_off) + q; };
-    int lane_gemm = 1;   // > 1: the GEMM launch below covers that many lanes
-    // the pre-split boundary GEMM: lane j's planes of operand r (0 = A, 1 = B) and scale words
-    const bool planes_on = planes_active(P);
-    auto planes_ptr = [&](int j, int r) {
-      return reinterpret_cast<_Float16*>((char*)P.d_planes + (size_t)j * P.planes_lane_bytes +
-                                         (r ? (size_t)12 * P.planes_n[0] : 0));
-    };
-    auto planes_sc = [&](int j, int r) {
-      return reinterpret_cast<int32_t*>((char*)P.d_planes + P.planes_sc_off) + 2 * j + r;
-    };
-    auto launch_one = [&](const Op& op, hipStream_t st) -> int {
-      const double beta = op.writes_output ? beta_out : 0.0;
-      if (planes_on && op.kind == OP_GEMM && &op == &P.ops[P.planes_gemm]) {
-        // lane batch: entries = the batch's lanes (planes and scale words at their lane strides),
-        // the combine sums them into lane 0's result when the plan sums the lanes (Op::lane_sum)
-        const int j0 = lane_gemm > 1 ? 0 : cur;
-        PlanesGemmArgs a;
-        a.A = planes_ptr(j0, 0);
-        a.B = planes_ptr(j0, 1);
-        a.sA = a.sB = (int64_t)(P.planes_lane_bytes / 2);
-        a.psA = P.planes_n[0];
-        a.psB = P.planes_n[1];
-        a.lda = op.lda;
-        a.ldb = op.ldb;
-        a.M = (int)op.M;
-        a.N = (int)op.N;
-        a.K = op.K;
-        a.batch = lane_gemm;
-        a.W = reinterpret_cast<float*>((char*)P.d_planes + P.planes_ws_off);
-        a.ws_bytes = P.planes_sc_off - P.planes_ws_off;
-        PlanesCombineArgs c;
-        c.sc_a = planes_sc(j0, 0);
-        c.sc_b = planes_sc(j0, 1);
-        c.sc_stride = 2;
-        c.C = ptr(op.c);
-        c.ldc = op.ldc;
-        c.sC = (int64_t)(P.lane_stride / esz);
-        c.lane_sum = lane_gemm > 1 && op.lane_sum;
-        c.beta = (float)beta;
-        return planes_gemm_launch(a, c, st);
+      GemmPresplit ps;
+      const bool pre = P.run_mode && op.ps_cand;
+      if (pre) {
+        ps.sc_a = sc_word(x, op.amax_a);
+        ps.sc_b = sc_word(x, op.amax_b);
+        ps.bad = bad_word(x, x.lane_sl[x.cur]);
       }
-      switch (op.kind) {
-        case OP_PERMUTE:
-          TQ_TRY(perm_plan_launch(P.perms[op.perm], (char*)P.d_tables + P.perm_tab_off[op.perm],
-                                  ptr(op.a), ptr(op.c), beta, st));
-          break;
-        case OP_GEMM: {
-          if (op.skinny) {
-            SkinnyArgs a = op.sk;
-            a.A = ptr(op.a);
-            a.B = ptr(op.b);
-            a.C = ptr(op.c);
-            a.W = op.ws_bytes ? ptr(op.ws) : nullptr;
-            a.beta = beta;
-            TQ_TRY(skinny_strided_launch(P.dtype, a, st));
-            break;
+      if (lane_gemm_ > 1) {   // every lane of the batch in one launch (Op::lane_batch)
+        const int64_t ls = (int64_t)(P.lane_stride / P.esz);
+        // pre-split: one window flag for the batch, in its first slice's word
+        TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, lane_gemm_, ptr(x, op.a), op.lda,
+                           op.a.kind == BUF_ARENA ? ls : 0, ptr(x, op.b), op.ldb, op.b.kind == BUF_ARENA ? ls : 0,
+                           beta, ptr(x, op.c), op.ldc, ls, (char*)P.d_arena + P.lane_ws_off, P.lane_ws_bytes, st,
+                           op.amax_a >= 0 ? amax_word(x, op.amax_a) : nullptr,
+                           op.amax_b >= 0 ? amax_word(x, op.amax_b) : nullptr, pre ? &ps : nullptr,
+                           op.amax_a >= 0 ? lane_amax_stride(x, op.amax_a) : 0,
+                           op.amax_b >= 0 ? lane_amax_stride(x, op.amax_b) : 0));
+        break;
+      }
+      TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(x, op.a), op.lda, op.sA,
+                         ptr(x, op.b), op.ldb, op.sB, beta, ptr(x, op.c), op.ldc, op.sC,
+                         op.ws_bytes ? ptr(x, op.ws) : nullptr, op.ws_bytes, st,
+                         op.amax_a >= 0 ? amax_lane(x, op.amax_a, x.cur) : nullptr,
+                         op.amax_b >= 0 ? amax_lane(x, op.amax_b, x.cur) : nullptr, pre ? &ps : nullptr));
+      break;
+    }
+    case OP_APPLY:
+      TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.M, op.K2, op.I, op.N, ptr(x, op.a), ptr(x, op.b),
+                          op.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[op.gtab]) : nullptr,
+                          ptr(x, op.c), beta, st));
+      break;
+    case OP_AXPY:
+      TQ_TRY(axpy_launch(P.dtype, op.n, ptr(x, op.a), ptr(x, op.c), beta, st));
+      break;
+    case OP_SWEEP: {
+      SweepArgs a;
+      const char* blob = (const char*)P.d_tables + P.stab_off[op.stab];
+      a.X = ptr(x, op.a);
+      a.Y = ptr(x, op.c);
+      a.ncols = op.ncols;
+      auto lg = [](int64_t v) {
+        if (v <= 0 || (v & (v - 1))) return -1;
+        int l = 0;
+        while ((int64_t(1) << l) < v) ++l;
+        return l;
+      };
+      a.nruns = op.nruns;
+      for (int r = 0; r < op.nruns; ++r) {
+        a.run_ext[r] = op.run_ext[r]; a.run_in[r] = op.run_in[r]; a.run_out[r] = op.run_out[r];
+        a.run_shift[r] = lg(op.run_ext[r]);
+      }
+      a.tin = op.tin;
+      a.tout = op.tout;
+      a.tin_shift = lg(op.tin);
+      a.tout_shift = lg(op.tout);
+      a.tabs = (const int32_t*)(blob + op.tabs_at);
+      a.tab_len = op.tab_len;
+      a.tin_off = (const int64_t*)blob;
+      a.tout_off = (const int64_t*)(blob + op.tout_off_at);
+      a.ngates = (int)op.sgates.size();
+      for (int j = 0; j < a.ngates; ++j) {
+        const SweepGate& g = op.sgates[j];
+        a.G[j] = ptr(x, g.g);
+        a.gidx[j] = g.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[g.gtab]) : nullptr;
+        a.K[j] = g.K; a.N[j] = g.N; a.W[j] = g.W;
+        a.tab_at[j] = (int)g.tab_off;
+      }
+      // power-of-two outer extents: per-bit column-offset weights
+      {
+        bool p2 = true;
+        int nb = 0;
+        for (int r = 0; r < op.nruns && p2; ++r) {
+          const int l = lg(op.run_ext[r]);
+          if (l < 0 || nb + l > 48) { p2 = false; break; }
+          for (int b = 0; b < l; ++b) {
+            a.w_in[nb + b] = op.run_in[r] << b;
+            a.w_out[nb + b] = op.run_out[r] << b;
           }
-          GemmPresplit ps;
-          const bool pre = P.run_mode && op.ps_cand;
-          if (pre) {
-            ps.sc_a = sc_word(op.amax_a);
-            ps.sc_b = sc_word(op.amax_b);
-            ps.bad = bad_word(lane_sl[cur]);
-          }
-          if (lane_gemm > 1) {   // every lane of the batch in one launch (Op::lane_batch)
-            const int64_t ls = (int64_t)(P.lane_stride / esz);
-            // pre-split: one window flag for the batch, in its first slice's word
-            TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, lane_gemm, ptr(op.a),
-                               op.lda, op.a.kind == BUF_ARENA ? ls : 0, ptr(op.b), op.ldb,
-                               op.b.kind == BUF_ARENA ? ls : 0, beta, ptr(op.c), op.ldc, ls,
-                               (char*)P.d_arena + P.lane_ws_off, P.lane_ws_bytes, st,
-                               op.amax_a >= 0 ? amax_word(op.amax_a) : nullptr,
-                               op.amax_b >= 0 ? amax_word(op.amax_b) : nullptr, pre ? &ps : nullptr,
-                               op.amax_a >= 0 ? lane_amax_stride(op.amax_a) : 0,
-                               op.amax_b >= 0 ? lane_amax_stride(op.amax_b) : 0));
-            break;
-          }
-          TQ_TRY(gemm_launch(P.dtype, op.transA, op.transB, op.M, op.N, op.K, op.batch, ptr(op.a),
-                             op.lda, op.sA, ptr(op.b), op.ldb, op.sB, beta, ptr(op.c), op.ldc, op.sC,
-                             op.ws_bytes ? ptr(op.ws) : nullptr, op.ws_bytes, st,
-                             op.amax_a >= 0 ? amax_lane(op.amax_a, cur) : nullptr,
-                             op.amax_b >= 0 ? amax_lane(op.amax_b, cur) : nullptr, pre ? &ps : nullptr));
-          break;
+          nb += l;
         }
-        case OP_APPLY:
-          TQ_TRY(apply_launch(P.dtype, op.O, op.K, op.M, op.K2, op.I, op.N, ptr(op.a), ptr(op.b),
-                              op.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[op.gtab]) : nullptr,
-                              ptr(op.c), beta, st));
-          break;
-        case OP_AXPY:
-          TQ_TRY(axpy_launch(P.dtype, op.n, ptr(op.a), ptr(op.c), beta, st));
-          break;
-        case OP_SWEEP: {
-          SweepArgs a;
-          const char* blob = (const char*)P.d_tables + P.stab_off[op.stab];
-          a.X = ptr(op.a);
-          a.Y = ptr(op.c);
-          a.ncols = op.ncols;
-          auto lg = [](int64_t v) {
-            if (v <= 0 || (v & (v - 1))) return -1;
-            int l = 0;
-            while ((int64_t(1) << l) < v) ++l;
-            return l;
-          };
-          a.nruns = op.nruns;
-          for (int r = 0; r < op.nruns; ++r) {
-            a.run_ext[r] = op.run_ext[r]; a.run_in[r] = op.run_in[r]; a.run_out[r] = op.run_out[r];
-            a.run_shift[r] = lg(op.run_ext[r]);
-          }
-          a.tin = op.tin;
-          a.tout = op.tout;
-          a.tin_shift = lg(op.tin);
-          a.tout_shift = lg(op.tout);
-          a.tabs = (const int32_t*)(blob + op.tabs_at);
-          a.tab_len = op.tab_len;
-          a.tin_off = (const int64_t*)blob;
-          a.tout_off = (const int64_t*)(blob + op.tout_off_at);
-          a.ngates = (int)op.sgates.size();
-          for (int j = 0; j < a.ngates; ++j) {
-            const SweepGate& g = op.sgates[j];
-            a.G[j] = ptr(g.g);
-            a.gidx[j] = g.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[g.gtab]) : nullptr;
-            a.K[j] = g.K; a.N[j] = g.N; a.W[j] = g.W;
-            a.tab_at[j] = (int)g.tab_off;
-          }
-          // power-of-two outer extents: per-bit column-offset weights
-          {
-            bool p2 = true;
-            int nb = 0;
-            for (int r = 0; r < op.nruns && p2; ++r) {
-              const int l = lg(op.run_ext[r]);
-              if (l < 0 || nb + l > 48) { p2 = false; break; }
-              for (int b = 0; b < l; ++b) {
-                a.w_in[nb + b] = op.run_in[r] << b;
-                a.w_out[nb + b] = op.run_out[r] << b;
-              }
-              nb += l;
-            }
-            a.colbits = p2 ? nb : -1;
-          }
-          a.load_colfast = op.load_colfast;
-          a.store_colfast = op.store_colfast;
-          a.use_beta = beta != 0.0;
-          a.beta = beta;
-          TQ_TRY(sweep_launch(P.dtype, a, st));
-          break;
-        }
-        default:
-          set_error("internal: op kind");
-          return TQ_ERR_INVALID;
+        a.colbits = p2 ? nb : -1;
       }
-      return TQ_OK;
-    };
-    // a sweep2 op's launch record from descriptor stabs[stab] (the current lane's pointers)
-    auto fill_s2 = [&](S2Op& o, const Op& op, int stab) -> int {
-      o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[stab]);
-      o.X = ptr(op.a);
-      o.Y = ptr(op.c);
-      const S2Desc* hd = reinterpret_cast<const S2Desc*>(P.stabs[stab].data());
-      for (size_t g = 0; g < op.sgates.size(); ++g) {
-        o.G[g] = ptr(op.sgates[g].g);
-        int mx = 0;
-        for (int t = 0; t < hd->gate[g].K * hd->gate[g].N; ++t) mx = std::max(mx, hd->gate[g].gidx[t] + 1);
-        if (mx > kS2GateRaw) { set_error("internal: sweep2 gate tensor too large"); return TQ_ERR_INVALID; }
-        o.gnum[g] = (uint8_t)mx;
-      }
-      o.beta = op.writes_output ? beta_out : 0.0;
-      o.use_beta = o.beta != 0.0;
-      o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
-      o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
-      return TQ_OK;
-    };
-    // Plan::seq_once run [b, e): its ops in order, a workgroup per stream, one launch; or
-    // (coop >= 0) Plan::coop_once run `coop`: its ops in order on coop_width workgroups each
-    auto launch_chain = [&](int b, int e, int coop) -> int {
+      a.load_colfast = op.load_colfast;
+      a.store_colfast = op.store_colfast;
+      a.use_beta = beta != 0.0;
+      a.beta = beta;
+      TQ_TRY(sweep_launch(P.dtype, a, st));
+      break;
+    }
+    default:
+      set_error("internal: op kind");
+      return TQ_ERR_INVALID;
+  }
+  return TQ_OK;
+}
+
+// a sweep2 op's launch record from descriptor stabs[stab] (the instance's current lane)
+int Exec::fill_s2(const Inst& x, S2Op& o, const Op& op, int stab) const {
+  const Plan& P = *x.P;
+  o.desc = (const S2Desc*)((const char*)P.d_tables + P.stab_off[stab]);
+  o.X = ptr(x, op.a);
+  o.Y = ptr(x, op.c);
+  const S2Desc* hd = reinterpret_cast<const S2Desc*>(P.stabs[stab].data());
+  for (size_t g = 0; g < op.sgates.size(); ++g) {
+    o.G[g] = ptr(x, op.sgates[g].g);
+    int mx = 0;
+    for (int t = 0; t < hd->gate[g].K * hd->gate[g].N; ++t) mx = std::max(mx, hd->gate[g].gidx[t] + 1);
+    if (mx > kS2GateRaw) {
+      set_error("internal: sweep2 gate tensor too large");
+      return TQ_ERR_INVALID;
+    }
+    o.gnum[g] = (uint8_t)mx;
+  }
+  o.beta = op.writes_output ? x.beta_out : 0.0;
+  o.use_beta = o.beta != 0.0;
+  o.amax = op.amax_word >= 0 ? amax_lane(x, op.amax_word, x.cur) : nullptr;
+  o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(x, op.amax_word) : nullptr;
+  return TQ_OK;
+}
+
+// Plan::seq_once run [b, e): its ops in order, a workgroup per (instance, stream), one launch (as
+// many instances per launch as kS2SeqMaxStreams allows); or (coop >= 0) Plan::coop_once run
+// `coop`: its ops in order on coop_width workgroups each, one launch per instance
+int Exec::launch_chain(int b, int e, int coop) {
+  const bool prof = (P0_.profile >> (int)OP_SWEEP) & 1;
+  if (coop >= 0) {
+    for (auto& x : I_) {
+      Plan& P = *x.P;
       Plan::Ev ev{};
-      const bool prof = (P.profile >> (int)OP_SWEEP) & 1;
       if (prof) {
-        if (P.ev_free.empty()) {
-          TQ_HIP(hipEventCreate(&ev.a));
-          TQ_HIP(hipEventCreate(&ev.b));
-        } else {
-          ev = P.ev_free.back();
-          P.ev_free.pop_back();
-        }
-        ev.kind = (int)OP_SWEEP; ev.flops = 0; ev.bytes = 0;
-        TQ_HIP(hipEventRecord(ev.a, stream));
+        ev = ev_begin((int)OP_SWEEP);
+        TQ_HIP(hipEventRecord(ev.a, st_));
       }
+      const int w = P.coop_width[coop];
       S2Launch L;
       L.seq = 1;
-      if (coop >= 0) {
-        const int w = P.coop_width[coop];
-        L.sync = reinterpret_cast<uint32_t*>((char*)P.d_tables + P.sync_off + (size_t)coop * Plan::kSyncSlot);
-        for (int i = b; i < e; ++i) {
-          const Op& op = P.ops[P.sched_once[i][0]];
-          S2Op& o = L.op[L.nops];
-          TQ_TRY(fill_s2(o, op, op.stab));
-          o.block_begin = 0;
-          o.nblocks = w;
-          o.lds_io = kS2Coop | (L.nops * w) << 8 | (op.lds_io & 4);   // (bit 2: set by the planner)
-          ++L.nops;
-          ev.flops += op.flops;
-          ev.bytes += op.bytes;
-        }
-        L.sync_total = L.nops * w;
-        TQ_TRY(sweep2_launch(P.dtype, L, stream));
-        if (prof) {
-          TQ_HIP(hipEventRecord(ev.b, stream));
-          P.ev_used.push_back(ev);
-        }
-        return TQ_OK;
+      L.sync = reinterpret_cast<uint32_t*>((char*)P.d_tables + P.sync_off + (size_t)coop * Plan::kSyncSlot);
+      for (int i = b; i < e; ++i) {
+        const Op& op = P.ops[P.sched_once[i][0]];
+        S2Op& o = L.op[L.nops];
+        TQ_TRY(fill_s2(x, o, op, op.stab));
+        o.block_begin = 0;
+        o.nblocks = w;
+        o.lds_io = kS2Coop | (L.nops * w) << 8 | (op.lds_io & 4);   // (bit 2: set by the planner)
+        ++L.nops;
+        ev.flops += op.flops;
+        ev.bytes += op.bytes;
       }
+      L.sync_total = L.nops * w;
+      TQ_TRY(sweep2_launch(P.dtype, L, st_));
+      if (prof) {
+        TQ_HIP(hipEventRecord(ev.b, st_));
+        P0_.ev_used.push_back(ev);
+      }
+    }
+    return TQ_OK;
+  }
+  int nstreams = 1, nops = 0;
+  for (int i = b; i < e; ++i)
+    for (int j : P0_.sched_once[i]) {
+      nstreams = std::max(nstreams, P0_.seq_stream[j] + 1);
+      ++nops;
+    }
+  const int per = std::max(1, std::min(kS2SeqMaxStreams / nstreams, kS2MaxOps / std::max(1, nops)));
+  for (size_t k0 = 0; k0 < I_.size(); k0 += (size_t)per) {
+    Plan::Ev ev{};
+    if (prof) {
+      ev = ev_begin((int)OP_SWEEP);
+      TQ_HIP(hipEventRecord(ev.a, st_));
+    }
+    S2Launch L;
+    L.seq = 1;
+    for (size_t k = k0; k < std::min(I_.size(), k0 + (size_t)per); ++k) {
+      const Inst& x = I_[k];
+      const Plan& P = *x.P;
       for (int i = b; i < e; ++i)
         for (int j : P.sched_once[i]) {
           const Op& op = P.ops[j];
           S2Op& o = L.op[L.nops++];
-          TQ_TRY(fill_s2(o, op, op.stab1));
+          TQ_TRY(fill_s2(x, o, op, op.stab1));
           o.lds_io = op.lds_io;
           // an LDS hand-off moves the whole tensor: the kernel's first-chunk path only
           if ((o.lds_io & 3) && reinterpret_cast<const S2Desc*>(P.stabs[op.stab1].data())->nchunks != 1) {
             set_error("internal: sweep2 LDS hand-off on a multi-chunk layout");
             return TQ_ERR_INVALID;
           }
-          o.block_begin = P.seq_stream[j];   // the stream's workgroup
+          o.block_begin = (int)(k - k0) * nstreams + P.seq_stream[j];   // the (instance, stream) workgroup
           o.nblocks = 1;
           ev.flops += op.flops;
           ev.bytes += op.bytes;
         }
-      TQ_TRY(sweep2_launch(P.dtype, L, stream));
-      if (prof) {
-        TQ_HIP(hipEventRecord(ev.b, stream));
-        P.ev_used.push_back(ev);
+    }
+    TQ_TRY(sweep2_launch(P0_.dtype, L, st_));
+    if (prof) {
+      TQ_HIP(hipEventRecord(ev.b, st_));
+      P0_.ev_used.push_back(ev);
+    }
+  }
+  return TQ_OK;
+}
+
+// one entry of the schedule: a single op (per instance), or independent sweep2 ops of every
+// instance (and, merged across the batch, of every lane) in one launch
+int Exec::launch(const std::vector<int>& grp) {
+  const Op& op0 = P0_.ops[grp[0]];
+  const int pkind = op0.kind == OP_SWEEP2 ? (int)OP_SWEEP : op0.kind;
+  const int nl = (int)I_[0].lane_sl.size();
+  Plan::Ev ev{};
+  const bool prof = (P0_.profile >> pkind) & 1;
+  bool lanes_merge = op0.kind == OP_SWEEP2 && nl > 1 && !op0.invariant;
+  for (int j : grp) lanes_merge = lanes_merge && !P0_.ops[j].writes_output;
+  if (prof) {
+    ev = ev_begin(pkind);
+    // a lane-batched GEMM or a sweep level merged across the batch's lanes does every lane's
+    // work; a group does every instance's
+    const int mult = (lanes_merge ? nl : lane_gemm_) * (int)I_.size();
+    for (int j : grp) {
+      ev.flops += P0_.ops[j].flops * mult;
+      ev.bytes += P0_.ops[j].bytes * mult;
+    }
+    TQ_HIP(hipEventRecord(ev.a, st_));
+  }
+  if (op0.kind == OP_SWEEP2) {
+    // (instance, lane, op) triples of this level: every lane's ops when the level is merged
+    // across the batch, else each instance's current lane; at most kS2MaxOps per launch
+    struct Item { int k, lane, q; };
+    std::vector<Item> items, dense;
+    for (int k = 0; k < (int)I_.size(); ++k)
+      for (int j = 0; j < (lanes_merge ? nl : 1); ++j)
+        for (int q : grp) (P0_.ops[q].s2_dense ? dense : items).push_back({k, lanes_merge ? j : I_[k].cur, q});
+    std::vector<int> keep(I_.size());
+    for (size_t k = 0; k < I_.size(); ++k) keep[k] = I_[k].cur;
+    // dense ops (tq_sweepd.hip): their own launches, at most two input tile sizes each
+    // (TQ_S2D_MIX=0: one)
+    static const bool s2d_mix = [] {
+      const char* e = getenv("TQ_S2D_MIX");
+      return !(e && e[0] == '0');
+    }();
+    static const bool s2d_nt = [] {
+      const char* e = getenv("TQ_S2D_NT");
+      return e && e[0] == '1';
+    }();
+    while (!dense.empty()) {
+      S2DLaunch L;
+      const int tin = P0_.ops[dense[0].q].tin;
+      int tin2 = 0;
+      std::vector<Item> rest;
+      int blocks = 0;
+      for (auto& it : dense) {
+        Inst& x = I_[it.k];
+        const Plan& P = *x.P;
+        const Op& op = P.ops[it.q];
+        if (op.tin != tin && tin2 == 0 && s2d_mix && !s2d_nt) tin2 = op.tin;
+        if ((op.tin != tin && op.tin != tin2) || L.nops == kS2MaxOps) {
+          rest.push_back(it);
+          continue;
+        }
+        set_lane(x, it.lane);
+        S2DOp& o = L.op[L.nops++];
+        o.desc = (const S2Dense*)((const char*)P.d_tables + P.stab_off[op.stab]);
+        o.X = ptr(x, op.a);
+        o.M = ptr(x, op.b);
+        o.Y = ptr(x, op.c);
+        o.tin = op.tin;
+        o.tout = op.tout;
+        o.block_begin = blocks;
+        o.nblocks = s2d_blocks(op.ncols);
+        o.ncols = op.ncols;
+        blocks += o.nblocks;
+        o.beta = op.writes_output ? x.beta_out : 0.0;
+        o.use_beta = o.beta != 0.0;
+        o.amax = op.amax_word >= 0 ? amax_lane(x, op.amax_word, x.cur) : nullptr;
+        o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(x, op.amax_word) : nullptr;
+        if (planes_active(P) && op.planes_role) {
+          o.planes = planes_ptr(x, x.cur, op.planes_role - 1);
+          o.pstride = P.planes_n[op.planes_role - 1];
+          o.amax_in = amax_lane(x, op.planes_in_amax, x.cur);
+          o.sc_out = planes_sc(x, x.cur, op.planes_role - 1);
+          o.amax = nullptr;
+        }
       }
-      return TQ_OK;
-    };
-    // one entry of the schedule: a single op, or independent sweep2 ops in one launch
-    auto launch = [&](const std::vector<int>& grp) -> int {
-      const Op& op0 = P.ops[grp[0]];
-      const int pkind = op0.kind == OP_SWEEP2 ? (int)OP_SWEEP : op0.kind;
-      Plan::Ev ev{};
-      const bool prof = (P.profile >> pkind) & 1;
-      if (prof) {
-        if (P.ev_free.empty()) {
-          TQ_HIP(hipEventCreate(&ev.a));
-          TQ_HIP(hipEventCreate(&ev.b));
-        } else {
-          ev = P.ev_free.back();
-          P.ev_free.pop_back();
-        }
-        ev.kind = pkind; ev.flops = 0; ev.bytes = 0;
-        // a lane-batched GEMM or a sweep level merged across the batch's lanes does every lane's work
-        int mult = lane_gemm;
-        if (op0.kind == OP_SWEEP2 && lane_sl.size() > 1 && !op0.invariant) {
-          bool m = true;
-          for (int j : grp) m = m && !P.ops[j].writes_output;
-          if (m) mult = (int)lane_sl.size();
-        }
-        for (int j : grp) { ev.flops += P.ops[j].flops * mult; ev.bytes += P.ops[j].bytes * mult; }
-        TQ_HIP(hipEventRecord(ev.a, stream));
+      TQ_TRY(sweepd_launch(P0_.dtype, L, st_));
+      dense.swap(rest);
+    }
+    for (size_t i0 = 0; i0 < items.size(); i0 += kS2MaxOps) {
+      S2Launch L;
+      L.nops = (int)std::min<size_t>(kS2MaxOps, items.size() - i0);
+      int blocks = 0;
+      for (int q = 0; q < L.nops; ++q) {
+        const Item& it = items[i0 + q];
+        Inst& x = I_[it.k];
+        set_lane(x, it.lane);
+        const Op& op = x.P->ops[it.q];
+        S2Op& o = L.op[q];
+        TQ_TRY(fill_s2(x, o, op, op.stab));
+        o.block_begin = blocks;
+        o.nblocks = s2_blocks(op.s2_nchunks);
+        blocks += o.nblocks;
       }
-      bool lanes_merge = op0.kind == OP_SWEEP2 && lane_sl.size() > 1 && !op0.invariant;
-      for (int j : grp) lanes_merge = lanes_merge && !P.ops[j].writes_output;
-      if (op0.kind == OP_SWEEP2) {
-        // (lane, op) pairs of this level: every lane's ops when the level is merged across the
-        // batch, else the current lane's; at most kS2MaxOps per launch
-        std::vector<std::pair<int, int>> items, dense;
-        for (int j = 0; j < (lanes_merge ? (int)lane_sl.size() : 1); ++j)
-          for (int q : grp) (P.ops[q].s2_dense ? dense : items).push_back({lanes_merge ? j : cur, q});
-        const int keep = cur;
-        // dense ops (tq_sweepd.hip): their own launches, at most two input tile sizes each
-        // (TQ_S2D_MIX=0: one)
-        static const bool s2d_mix = [] {
-          const char* e = getenv("TQ_S2D_MIX");
-          return !(e && e[0] == '0');
-        }();
-        static const bool s2d_nt = [] {
-          const char* e = getenv("TQ_S2D_NT");
-          return e && e[0] == '1';
-        }();
-        while (!dense.empty()) {
-          S2DLaunch L;
-          const int tin = P.ops[dense[0].second].tin;
-          int tin2 = 0;
-          std::vector<std::pair<int, int>> rest;
-          int blocks = 0;
-          for (auto& it : dense) {
-            const Op& op = P.ops[it.second];
-            if (op.tin != tin && tin2 == 0 && s2d_mix && !s2d_nt) tin2 = op.tin;
-            if ((op.tin != tin && op.tin != tin2) || L.nops == kS2MaxOps) { rest.push_back(it); continue; }
-            set_lane(it.first);
-            S2DOp& o = L.op[L.nops++];
-            o.desc = (const S2Dense*)((const char*)P.d_tables + P.stab_off[op.stab]);
-            o.X = ptr(op.a);
-            o.M = ptr(op.b);
-            o.Y = ptr(op.c);
-            o.tin = op.tin;
-            o.tout = op.tout;
-            o.block_begin = blocks;
-            o.nblocks = s2d_blocks(op.ncols);
-            o.ncols = op.ncols;
-            blocks += o.nblocks;
-            o.beta = op.writes_output ? beta_out : 0.0;
-            o.use_beta = o.beta != 0.0;
-            o.amax = op.amax_word >= 0 ? amax_lane(op.amax_word, cur) : nullptr;
-            o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(op.amax_word) : nullptr;
-            if (planes_on && op.planes_role) {
-              o.planes = planes_ptr(cur, op.planes_role - 1);
-              o.pstride = P.planes_n[op.planes_role - 1];
-              o.amax_in = amax_lane(op.planes_in_amax, cur);
-              o.sc_out = planes_sc(cur, op.planes_role - 1);
-              o.amax = nullptr;
-            }
-          }
-          TQ_TRY(sweepd_launch(P.dtype, L, stream));
-          dense.swap(rest);
+      TQ_TRY(sweep2_launch(P0_.dtype, L, st_));
+    }
+    for (size_t k = 0; k < I_.size(); ++k) set_lane(I_[k], keep[k]);
+  } else {
+    for (auto& x : I_) TQ_TRY(launch_one(x, x.P->ops[grp[0]]));
+  }
+  if (prof) {
+    TQ_HIP(hipEventRecord(ev.b, st_));
+    P0_.ev_used.push_back(ev);
+  }
+  return TQ_OK;
+}
+
+int Exec::run(int64_t s_begin, int64_t s_end, int64_t s_step, int accumulate) {
+  const int ns = (int)P0_.sliced.size();
+  for (auto& x : I_) x.first = !accumulate;
+  if (s_begin >= s_end) {
+    for (auto& x : I_)
+      if (!accumulate && x.P->out_numel) TQ_HIP(hipMemsetAsync(x.out, 0, x.P->out_numel * esz(), st_));
+    return TQ_OK;
+  }
+  // Slices run in batches of P.lanes (slice lanes, Plan::lanes): lane j owns its own copy of the
+  // per-slice arena part, the batch's sweep2 levels share launches across lanes, other ops run
+  // lane by lane in lane order (so output accumulation keeps its order)
+  const int64_t nlanes = std::max(1, P0_.lanes);
+  std::vector<int64_t> in_off;
+  for (int64_t s0 = s_begin; s0 < s_end; s0 += s_step * nlanes) {
+    for (auto& x : I_) {
+      const Plan& P = *x.P;
+      x.lane_sl.clear();
+      x.lane_in_off.clear();
+      in_off.assign(P.n_inputs, 0);
+      for (int64_t sl = s0; sl < s_end && (int64_t)x.lane_sl.size() < nlanes; sl += s_step) {
+        // decode slice id (row-major over sliced modes) -> per-input element offsets
+        std::vector<int64_t> idx(ns);
+        int64_t rem = sl;
+        for (int q = ns - 1; q >= 0; --q) {
+          idx[q] = rem % P.sliced_ext[q];
+          rem /= P.sliced_ext[q];
         }
-        for (size_t i0 = 0; i0 < items.size(); i0 += kS2MaxOps) {
-        S2Launch L;
-        L.nops = (int)std::min<size_t>(kS2MaxOps, items.size() - i0);
-        int blocks = 0;
-        for (int q = 0; q < L.nops; ++q) {
-          set_lane(items[i0 + q].first);
-          const Op& op = P.ops[items[i0 + q].second];
-          S2Op& o = L.op[q];
-          TQ_TRY(fill_s2(o, op, op.stab));
-          o.block_begin = blocks;
-          o.nblocks = s2_blocks(op.s2_nchunks);
-          blocks += o.nblocks;
+        for (int i = 0; i < P.n_inputs; ++i) {
+          int64_t o = 0;
+          for (int q = 0; q < ns; ++q) o += idx[q] * P.inputs[i].slice_stride[q];
+          in_off[i] = o;
         }
-        TQ_TRY(sweep2_launch(P.dtype, L, stream));
-        }
-        set_lane(keep);
-      } else {
-        TQ_TRY(launch_one(op0, stream));
+        x.lane_sl.push_back(sl);
+        x.lane_in_off.push_back(in_off);
       }
-      if (prof) {
-        TQ_HIP(hipEventRecord(ev.b, stream));
-        P.ev_used.push_back(ev);
-      }
-      return TQ_OK;
-    };
-    if (sl == s_begin) {
-      if (P.n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(0), 0, P.n_amax_once * sizeof(uint32_t), stream));
+      set_lane(x, 0);
+      x.lanes_summed = false;
+    }
+    const int nl = (int)I_[0].lane_sl.size();
+    if (s0 == s_begin) {
+      for (auto& x : I_)
+        if (x.P->n_amax_once) TQ_HIP(hipMemsetAsync(amax_word(x, 0), 0, x.P->n_amax_once * sizeof(uint32_t), st_));
       size_t run = 0, crun = 0;
-      for (int i = 0; i < (int)P.sched_once.size();) {
-        while (P.use_seq && run < P.seq_once.size() && P.seq_once[run].first < i) ++run;
-        if (P.use_seq && run < P.seq_once.size() && P.seq_once[run].first == i) {
-          TQ_TRY(launch_chain(i, P.seq_once[run].second, -1));
-          i = P.seq_once[run].second;
+      for (int i = 0; i < (int)P0_.sched_once.size();) {
+        while (P0_.use_seq && run < P0_.seq_once.size() && P0_.seq_once[run].first < i) ++run;
+        if (P0_.use_seq && run < P0_.seq_once.size() && P0_.seq_once[run].first == i) {
+          TQ_TRY(launch_chain(i, P0_.seq_once[run].second, -1));
+          i = P0_.seq_once[run].second;
           continue;
         }
-        while (P.use_coop && crun < P.coop_once.size() && P.coop_once[crun].first < i) ++crun;
-        if (P.use_coop && crun < P.coop_once.size() && P.coop_once[crun].first == i) {
-          TQ_TRY(launch_chain(i, P.coop_once[crun].second, (int)crun));
-          i = P.coop_once[crun].second;
+        while (P0_.use_coop && crun < P0_.coop_once.size() && P0_.coop_once[crun].first < i) ++crun;
+        if (P0_.use_coop && crun < P0_.coop_once.size() && P0_.coop_once[crun].first == i) {
+          TQ_TRY(launch_chain(i, P0_.coop_once[crun].second, (int)crun));
+          i = P0_.coop_once[crun].second;
           continue;
         }
-        TQ_TRY(launch(P.sched_once[i]));
+        TQ_TRY(launch(P0_.sched_once[i]));
         ++i;
       }
     }
     // per-slice max words: one set per lane (pre-split mode: one set shared by the batch's
     // lanes, max-ed over all of them -- an upper bound of every lane's operand)
-    if (P.n_amax_slice && P.run_mode)   // scales from the previous slice's max, then max = 0
-      TQ_TRY(presplit_prep_launch(amax_word(P.n_amax_once), sc_word(P.n_amax_once), P.n_amax_slice, stream));
-    else if (P.n_amax_slice)
-      TQ_HIP(hipMemsetAsync(amax_word(P.n_amax_once), 0,
-                            (size_t)P.n_amax_slice * lane_sl.size() * sizeof(uint32_t), stream));
-    bool lanes_summed = false;   // this batch's lanes were summed into lane 0 (Op::lane_sum)
-    for (auto& grp : P.sched_slice) {
-      const Op& op0 = P.ops[grp[0]];
+    for (auto& x : I_) {
+      const Plan& P = *x.P;
+      if (P.n_amax_slice && P.run_mode)   // scales from the previous slice's max, then max = 0
+        TQ_TRY(presplit_prep_launch(amax_word(x, P.n_amax_once), sc_word(x, P.n_amax_once), P.n_amax_slice, st_));
+      else if (P.n_amax_slice)
+        TQ_HIP(hipMemsetAsync(amax_word(x, P.n_amax_once), 0, (size_t)P.n_amax_slice * nl * sizeof(uint32_t), st_));
+    }
+    for (auto& grp : P0_.sched_slice) {
+      const Op& op0 = P0_.ops[grp[0]];
       bool merged = op0.kind == OP_SWEEP2;
-      for (int j : grp) merged = merged && !P.ops[j].writes_output;
-      if (merged || lane_sl.size() == 1) {
-        set_lane(0);
+      for (int j : grp) merged = merged && !P0_.ops[j].writes_output;
+      if (merged || nl == 1) {
+        set_lane_all(0);
         TQ_TRY(launch(grp));
-        if (merged && lane_sl.size() > 1)
-          for (int j : grp)
-            if (P.ops[j].lane_sum) {   // a lane-merged level whose lanes an output permute sums
-              TQ_TRY(lane_sum_launch(P.dtype, P.ops[j].nc, ptr(P.ops[j].c), (int64_t)(P.lane_stride / esz),
-                                     (int)lane_sl.size(), stream));
-              lanes_summed = true;
-            }
+        if (merged && nl > 1)
+          for (auto& x : I_)
+            for (int j : grp)
+              if (x.P->ops[j].lane_sum) {   // a lane-merged level whose lanes an output permute sums
+                TQ_TRY(lane_sum_launch(x.P->dtype, x.P->ops[j].nc, ptr(x, x.P->ops[j].c),
+                                       (int64_t)(x.P->lane_stride / esz()), nl, st_));
+                x.lanes_summed = true;
+              }
       } else if (op0.kind == OP_GEMM && op0.lane_batch) {
-        set_lane(0);
-        lane_gemm = (int)lane_sl.size();
-        const int rc = launch(grp);
-        lane_gemm = 1;
-        TQ_TRY(rc);
-        if (op0.lane_sum) {
-          // (the pre-split GEMM's combine has summed the lanes already)
-          if (!(planes_on && grp[0] == P.planes_gemm))
-            TQ_TRY(lane_sum_launch(P.dtype, op0.nc, ptr(op0.c), (int64_t)(P.lane_stride / esz),
-                                   (int)lane_sl.size(), stream));
-          lanes_summed = true;
+        set_lane_all(0);
+        lane_gemm_ = nl;
+        int rc = TQ_OK;
+        for (auto& x : I_) {
+          rc = launch_one(x, x.P->ops[grp[0]]);
+          if (rc != TQ_OK) break;
+          if (op0.lane_sum) {
+            // (the pre-split GEMM's combine has summed the lanes already)
+            if (!(planes_active(*x.P) && grp[0] == x.P->planes_gemm))
+              rc = lane_sum_launch(x.P->dtype, op0.nc, ptr(x, op0.c), (int64_t)(x.P->lane_stride / esz()), nl, st_);
+            x.lanes_summed = true;
+            if (rc != TQ_OK) break;
+          }
         }
-      } else if (op0.lane_once && lanes_summed) {
-        set_lane(0);
+        lane_gemm_ = 1;
+        TQ_TRY(rc);
+      } else if (op0.lane_once && I_[0].lanes_summed) {
+        set_lane_all(0);
         TQ_TRY(launch(grp));
       } else {
-        for (int j = 0; j < (int)lane_sl.size(); ++j) {
-          set_lane(j);
+        for (int j = 0; j < nl; ++j) {
+          set_lane_all(j);
           TQ_TRY(launch(grp));
         }
       }
     }
-    first = false;
+    for (auto& x : I_) x.first = false;
   }
+  return TQ_OK;
+}
+
+// the plans of a group are the same compiled network (identical op lists and schedules)
+bool same_structure(const Plan& a, const Plan& b) {
+  if (a.dtype != b.dtype || a.ops.size() != b.ops.size() || a.sched_once != b.sched_once ||
+      a.sched_slice != b.sched_slice || a.lanes != b.lanes || a.n_slices != b.n_slices ||
+      a.seq_once != b.seq_once || a.seq_stream != b.seq_stream || a.use_seq != b.use_seq ||
+      a.use_coop != b.use_coop || a.coop_once != b.coop_once || a.n_inputs != b.n_inputs ||
+      planes_active(a) != planes_active(b) || a.planes_gemm != b.planes_gemm)
+    return false;
+  for (size_t i = 0; i < a.ops.size(); ++i)
+    if (a.ops[i].kind != b.ops[i].kind || a.ops[i].stab != b.ops[i].stab || a.ops[i].stab1 != b.ops[i].stab1 ||
+        a.ops[i].invariant != b.ops[i].invariant || a.ops[i].writes_output != b.ops[i].writes_output)
+      return false;
+  return true;
+}
+
+}  // namespace
+
+int plan_enqueue(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
+                 int64_t s_step, int accumulate, hipStream_t stream) {
+  std::vector<Inst> I(1);
+  I[0].P = &P;
+  I[0].inputs = inputs;
+  I[0].out = out;
+  Exec ex(I, stream);
+  return ex.run(s_begin, s_end, s_step, accumulate);
+}
+
+int group_enqueue(Plan* const* plans, int n, const void* const* const* inputs, void* const* outs, int64_t s_begin,
+                  int64_t s_end, int64_t s_step, int accumulate, hipStream_t stream) {
+  std::vector<Inst> I((size_t)n);
+  for (int k = 0; k < n; ++k) {
+    I[k].P = plans[k];
+    I[k].inputs = inputs[k];
+    I[k].out = outs[k];
+  }
+  Exec ex(I, stream);
+  return ex.run(s_begin, s_end, s_step, accumulate);
+}
+
+uint64_t next_plan_serial() {
+  static std::atomic<uint64_t> c{0};
+  return ++c;
+}
+
+int plan_run_group(Plan* const* plans, int n, const void* const* const* inputs, void* const* outs, int64_t s_begin,
+                   int64_t s_end, int64_t s_step, int accumulate, hipStream_t stream) {
+  TQ_CHECK_ARG(n >= 1 && plans && inputs && outs, "empty group");
+  if (n == 1) return plan_run(*plans[0], inputs[0], outs[0], s_begin, s_end, s_step, accumulate, stream);
+  Plan& P0 = *plans[0];
+  TQ_CHECK_ARG(s_step >= 1, "slice_step");
+  TQ_CHECK_ARG(s_begin >= 0 && s_end <= P0.n_slices, "slice range");
+  int cur = -1;
+  TQ_HIP(hipGetDevice(&cur));
+  for (int k = 0; k < n; ++k) {
+    Plan& P = *plans[k];
+    TQ_CHECK_ARG(P.arena_bytes == 0 || P.d_arena, "plan not materialized");
+    TQ_CHECK_ARG(P.device < 0 || cur == P.device, "a group plan was materialized on another device");
+    for (int q = 0; q < k; ++q)
+      TQ_CHECK_ARG(plans[q] != plans[k] && outs[q] != outs[k], "a group runs distinct plans into distinct outputs");
+    P.run_mode = 0;   // no pre-split (predicted-scale) GEMM mode in a group
+    TQ_CHECK_ARG(same_structure(P0, P), "the plans of a group must be compiled from the same network");
+  }
+  TQ_CHECK_ARG(!P0.use_coop, "cooperative chain launches do not run in a group");
+  const bool eager = P0.profile || !P0.use_graph || graphs_disabled();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  TQ_HIP(hipStreamIsCapturing(stream, &cs));
+  if (eager || cs != hipStreamCaptureStatusNone)
+    return group_enqueue(plans, n, inputs, outs, s_begin, s_end, s_step, accumulate, stream);
+  // one hipGraph of the whole group, cached in the first plan under every member's serial,
+  // inputs and output (a serial is never reused, so a replay cannot address a freed plan)
+  Plan::GraphKey key;
+  for (int k = 0; k < n; ++k) {
+    key.inputs.insert(key.inputs.end(), inputs[k], inputs[k] + plans[k]->n_inputs);
+    key.group.push_back(outs[k]);
+    key.group.push_back(reinterpret_cast<const void*>((uintptr_t)plans[k]->serial));
+  }
+  key.out = outs[0]; key.b = s_begin; key.e = s_end; key.s = s_step; key.acc = accumulate;
+  key.planes = planes_active(P0) ? 1 : 0;
+  key.seq = P0.use_seq;
+  constexpr size_t kMaxGraphs = 8;
+  Plan::GraphEntry* hit = nullptr;
+  for (auto& g : P0.graphs) if (g.key == key) hit = &g;
+  if (!hit) {
+    if (P0.graphs.size() >= kMaxGraphs) {
+      auto lru = std::min_element(P0.graphs.begin(), P0.graphs.end(),
+                                  [](const Plan::GraphEntry& a, const Plan::GraphEntry& b) { return a.used < b.used; });
+      drop_graph_entry(*lru);
+      P0.graphs.erase(lru);
+    }
+    if (!P0.cap_stream) TQ_HIP(hipStreamCreateWithFlags(&P0.cap_stream, hipStreamNonBlocking));
+    TQ_HIP(hipStreamBeginCapture(P0.cap_stream, hipStreamCaptureModeThreadLocal));
+    const int rc = group_enqueue(plans, n, inputs, outs, s_begin, s_end, s_step, accumulate, P0.cap_stream);
+    hipGraph_t g = nullptr;
+    const hipError_t ce = hipStreamEndCapture(P0.cap_stream, &g);
+    if (rc != TQ_OK) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    TQ_HIP(ce);
+    Plan::GraphEntry e;
+    e.key = key;
+    e.graph = g;
+    TQ_HIP(hipGraphInstantiate(&e.exec, g, nullptr, nullptr, 0));
+    TQ_HIP(hipEventCreateWithFlags(&e.done, hipEventDisableTiming));
+    P0.graphs.push_back(e);
+    hit = &P0.graphs.back();
+    ++P0.graph_builds;
+  }
+  hit->used = ++P0.graph_clock;
+  TQ_HIP(hipGraphLaunch(hit->exec, stream));
+  TQ_HIP(hipEventRecord(hit->done, stream));
+  ++P0.graph_launches;
   return TQ_OK;
 }
 

@@ -168,6 +168,7 @@ struct Plan {
   void* d_tables = nullptr;
   bool owns_device = false;
   int device = -1;          // HIP device the arena / tables / graphs belong to (set at materialize)
+  uint64_t serial = 0;      // process-unique id (set at materialize; group graph keys)
   // optional per-op-kind timing with HIP events on the execution stream (bench evidence)
   unsigned profile = 0;  // bit k set: time ops of kind k
   struct Ev { hipEvent_t a, b; int kind; double flops, bytes; };
@@ -208,9 +209,11 @@ struct Plan {
     int planes = 0; // the pre-split boundary GEMM was on
     bool seq = true;  // Plan::use_seq
     bool coop = false;  // Plan::use_coop
+    // a group execute (plan_run_group): every member's output and serial
+    std::vector<const void*> group;
     bool operator==(const GraphKey& o) const {
       return inputs == o.inputs && out == o.out && b == o.b && e == o.e && s == o.s && acc == o.acc &&
-             mode == o.mode && seq == o.seq && coop == o.coop && planes == o.planes;
+             mode == o.mode && seq == o.seq && coop == o.coop && planes == o.planes && group == o.group;
     }
   };
   bool use_graph = true;
@@ -233,12 +236,20 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
                  const int64_t* in_extents, const int64_t* in_strides, int out_rank,
                  const int32_t* out_modes, int n_steps, const int32_t* path, int n_sliced,
                  const int32_t* sliced_modes);
+// a copy of a compiled plan without any device state (arena, tables, graphs, events): the
+// same schedule for another stream / block (tq_plan_clone)
+void plan_clone_compiled(const Plan& src, Plan& dst);
 // the pre-split boundary GEMM's buffer layout (planes, partials, scale words): host only
 void plan_planes_layout(Plan& P);
 // upload tables / allocate arena (owned) — or use caller memory when `arena`/`tables` are given
 int plan_materialize(Plan& P, void* arena, void* tables, hipStream_t stream);
 int plan_run(Plan& P, const void* const* inputs, void* out, int64_t s_begin, int64_t s_end,
              int64_t s_step, int accumulate, hipStream_t stream);
+// a group of plans compiled from the same network, run in lockstep on one stream: every sweep2 /
+// dense-sweep level and chain launch of all members is one launch (blocks as lanes); inputs[k] /
+// outs[k] are member k's.  Replayed as one hipGraph (cached in plans[0]).
+int plan_run_group(Plan* const* plans, int n, const void* const* const* inputs, void* const* outs,
+                   int64_t s_begin, int64_t s_end, int64_t s_step, int accumulate, hipStream_t stream);
 int plan_release(Plan& P);   // TQ_OK, or TQ_ERR_HIP with what is left still held (retry later)
 int plan_profile_read(Plan& P, int kind, double* ms, int64_t* launches, double* flops, double* bytes);
 

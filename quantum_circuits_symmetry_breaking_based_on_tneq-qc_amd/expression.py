@@ -56,6 +56,18 @@ class NativePlan:
     def query(self, key: str) -> int:
         return int(_lib.lib().tq_plan_query(self._h, key.encode()))
 
+    def clone(self) -> "NativePlan":
+        """A copy of this compiled plan with its own device state (arena, tables, graphs): one per
+        stream or block in flight, without compiling the network again (tq_plan_clone)."""
+        graphs.drain_deferred()
+        h = ctypes.c_void_p()
+        check(_lib.lib().tq_plan_clone(self._h, ctypes.byref(h)), "tq_plan_clone")
+        p = NativePlan.__new__(NativePlan)
+        p._h = h
+        p.dtype = self.dtype
+        p.n_slices = self.n_slices
+        return p
+
     def set(self, key: str, value: int) -> None:
         """Plan option (tq_plan_set): "graph" (replay a captured hipGraph, default 1),
         "sweep_chain" (chain launches of small dependent sweep2 ops, default 1), "sweep_coop"
@@ -84,6 +96,25 @@ class NativePlan:
         rc = _lib.lib().tq_plan_execute(self._h, arr, ctypes.c_void_p(out_ptr), begin, end, step,
                                         int(accumulate), ctypes.c_void_p(stream))
         check(rc, "tq_plan_execute")
+
+    @staticmethod
+    def execute_group(plans: Sequence["NativePlan"], ptr_arrays, out_ptrs: Sequence[int], stream: int,
+                      begin: int = 0, end: Optional[int] = None, step: int = 1, accumulate: bool = False) -> None:
+        """Run plans compiled from the same network in lockstep on one stream (blocks as lanes:
+        tq_plan_execute_group); ptr_arrays[k] / out_ptrs[k] are member k's inputs / output."""
+        n = len(plans)
+        if n == 0:
+            return
+        end = plans[0].n_slices if end is None else end
+        if graphs._DEFERRED:
+            graphs.drain_deferred()
+        hs = (ctypes.c_void_p * n)(*[p._h for p in plans])
+        arrs = [a if isinstance(a, ctypes.Array) else NativePlan.pointer_array(a) for a in ptr_arrays]
+        ins = (ctypes.POINTER(ctypes.c_void_p) * n)(*[ctypes.cast(a, ctypes.POINTER(ctypes.c_void_p)) for a in arrs])
+        outs = (ctypes.c_void_p * n)(*[int(o) for o in out_ptrs])
+        rc = _lib.lib().tq_plan_execute_group(n, hs, ins, outs, begin, end, step, int(accumulate),
+                                              ctypes.c_void_p(stream))
+        check(rc, "tq_plan_execute_group")
 
     def profile(self, kinds=-1) -> None:
         """Reset the records and time (HIP events on the execution stream) the op kinds in
@@ -202,6 +233,35 @@ class HipContractExpression:
         return p
 
     # -- execution ---------------------------------------------------------------------------
+    def bind(self, *tensors, private_plan: bool = False) -> "BoundOperands":
+        """Validate `tensors` once (shapes, device, dtype, strides) and return the plan bound to
+        their storage.  The binding reads whatever values those tensors hold when it runs, so an
+        owner that updates operand VALUES in place (a sampler's projector vectors) runs it again
+        without re-validation; the tensors themselves must stay alive and keep their storage,
+        shapes and strides (the binding holds references to them).  `private_plan`: a clone of
+        the expression's plan owned by this binding (one per stream / block in flight)."""
+        if len(tensors) != len(self.net.terms):
+            raise ValueError(f"expression takes {len(self.net.terms)} operands, got {len(tensors)}")
+        ts = list(tensors)
+        for t, s in zip(ts, self.shapes):
+            if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+                raise ValueError("bind() takes device tensors")
+            if tuple(t.shape) != s:
+                raise ValueError(f"operand shape {tuple(t.shape)} does not match expression shape {s}")
+            if t.is_conj() or t.is_neg() or any(st < 0 for st in t.stride()):
+                raise ValueError("bind() takes plain (non-conjugated, non-negative-stride) tensors")
+        dt = ts[0].dtype
+        dev = ts[0].device
+        for t in ts:
+            if t.dtype != dt or t.device != dev:
+                raise ValueError("bind() takes operands of one dtype on one device")
+        dtype_code(dt)
+        contiguous = all(t.is_contiguous() for t in ts)
+        plan = self.plan(dt, None if contiguous else [t.stride() for t in ts], dev.index)
+        if private_plan:
+            plan = plan.clone()
+        return BoundOperands(self, plan, plan.pointer_array([t.data_ptr() for t in ts]), tuple(ts), dev, dt)
+
     def __call__(self, *tensors, out: Optional[torch.Tensor] = None, slice_range=None,
                  accumulate: bool = False, backend=None) -> torch.Tensor:
         if (torch.is_grad_enabled() and out is None
@@ -370,6 +430,53 @@ class HipContractExpression:
             stream = torch.cuda.current_stream(dev).cuda_stream
             plan.execute(arr, out.data_ptr(), stream, begin, end, step, accumulate)
         return out
+
+
+class BoundOperands:
+    """An expression's native plan bound to fixed operand storage (HipContractExpression.bind)."""
+
+    __slots__ = ("expr", "plan", "arr", "tensors", "device", "dtype")
+
+    def __init__(self, expr, plan, arr, tensors, device, dtype):
+        self.expr, self.plan, self.arr, self.tensors, self.device, self.dtype = expr, plan, arr, tensors, device, dtype
+
+    def new_out(self) -> torch.Tensor:
+        return torch.empty(self.expr.out_shape, dtype=self.dtype, device=self.device)
+
+    def _check_out(self, out: torch.Tensor) -> None:
+        if (tuple(out.shape) != self.expr.out_shape or out.dtype != self.dtype or not out.is_contiguous()
+                or out.device != self.device):
+            raise ValueError("out tensor has the wrong shape/dtype/device or is not contiguous")
+
+    def run(self, out: torch.Tensor, stream: Optional[torch.cuda.Stream] = None, slice_range=None) -> torch.Tensor:
+        """Contract into `out` on `stream` (default: the current stream)."""
+        self._check_out(out)
+        begin, end, step = (0, self.plan.n_slices, 1) if slice_range is None else slice_range
+        s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        with torch.cuda.device(self.device):
+            self.plan.execute(self.arr, out.data_ptr(), s, begin, end, step, False)
+        return out
+
+
+def run_group(bound: Sequence[BoundOperands], outs: Sequence[torch.Tensor],
+              stream: Optional[torch.cuda.Stream] = None, slice_range=None) -> None:
+    """Contract every member of `bound` (one network, distinct plans: e.g. the same expression
+    compiled once per block) into its own output in ONE lockstep schedule (tq_plan_execute_group:
+    blocks as lanes)."""
+    if len(bound) != len(outs):
+        raise ValueError("one output per bound member")
+    if not bound:
+        return
+    for b, o in zip(bound, outs):
+        b._check_out(o)
+    plans = [b.plan for b in bound]
+    if len({id(p) for p in plans}) != len(plans):
+        raise ValueError("run_group members need distinct plans (one expression per member)")
+    dev = bound[0].device
+    begin, end, step = (0, plans[0].n_slices, 1) if slice_range is None else slice_range
+    s = (stream or torch.cuda.current_stream(dev)).cuda_stream
+    with torch.cuda.device(dev):
+        NativePlan.execute_group(plans, [b.arr for b in bound], [o.data_ptr() for o in outs], s, begin, end, step)
 
 
 def _in_place_order(mi, mj, res, ext):
