@@ -270,6 +270,15 @@ int tq_plan_set(tq_plan p, const char* key, int64_t value) {
     p->plan.use_planes = value != 0;
     return TQ_OK;
   }
+  if (k == "group_hint") {       // compile again for lockstep groups of `value` plans (before the first execute)
+    if (p->materialized) {
+      tq::set_error("tq_plan_set: group_hint before the plan's first execute only");
+      return TQ_ERR_INVALID;
+    }
+    TQ_GUARD_BEGIN
+    return tq::plan_recompile(p->plan, (int)value);
+    TQ_GUARD_END
+  }
   if (k == "sweep_coop") {       // 0: the multi-chunk sweep2 levels of a chain run one launch each
     p->plan.use_coop = value != 0;
     return TQ_OK;
@@ -297,6 +306,7 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "graph_launches") return P.graph_launches;
   if (k == "n_presplit") return P.n_ps;
   if (k == "lanes") return P.lanes;
+  if (k == "group_hint") return P.group_hint;
   if (k == "presplit_fallbacks") return P.ps_fallbacks;
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;

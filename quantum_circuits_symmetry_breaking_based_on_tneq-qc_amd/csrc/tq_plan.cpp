@@ -100,7 +100,10 @@ class Compiler {
  public:
   // lanes_hint > 1: the plan will run its slices in batches of that many lanes, so a
   // slice-dependent sweep op needs only min_chunks / lanes chunks to fill the GPU
-  Compiler(Plan& P, int lanes_hint = 1) : P_(P), lanes_hint_(lanes_hint) {}
+  // group_hint > 1: the plan will run in lockstep groups of that many plans (blocks as lanes,
+  // plan_run_group), so every sweep op shares its launches with group_hint - 1 others
+  Compiler(Plan& P, int lanes_hint = 1, int group_hint = 1)
+      : P_(P), lanes_hint_(lanes_hint), group_hint_(std::max(1, group_hint)) {}
 
   int run(int n_inputs, const int32_t* in_ranks, const int32_t* in_modes, const int64_t* in_ext,
           const int64_t* in_strides, int out_rank, const int32_t* out_modes, int n_steps,
@@ -1539,7 +1542,7 @@ class Compiler {
     lc = std::min(lc, d.colbits);
     // small tensors: narrower chunks, so that the op still spreads over >= s2_min_chunks()
     // workgroups (a 2^19-element tensor with a 256-element tile has only 64 chunks of 32 columns)
-    if (const int mc = (c.dep && lanes_hint_ > 1) ? std::max(1, s2_min_chunks() / lanes_hint_) : s2_min_chunks();
+    if (const int mc = std::max(1, s2_min_chunks() / (group_hint_ * ((c.dep && lanes_hint_ > 1) ? lanes_hint_ : 1)));
         mc > 1) {
       int lg = 0;
       while ((2 << lg) <= mc) ++lg;
@@ -2512,6 +2515,7 @@ class Compiler {
 
   Plan& P_;
   int lanes_hint_ = 1;
+  int group_hint_ = 1;
   bool one_chunk_ = false;   // s2_layout: one chunk of the whole tensor when it fits the tile
   bool cplx_ = false;
   int n_inputs_ = 0;
@@ -2532,15 +2536,16 @@ class Compiler {
 int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, const int32_t* in_modes,
                  const int64_t* in_extents, const int64_t* in_strides, int out_rank,
                  const int32_t* out_modes, int n_steps, const int32_t* path, int n_sliced,
-                 const int32_t* sliced_modes) {
+                 const int32_t* sliced_modes, int group_hint) {
   TQ_CHECK_ARG(dtype_valid(dtype), "dtype");
+  TQ_CHECK_ARG(group_hint >= 1, "group_hint");
   TQ_CHECK_ARG(n_inputs >= 1, "need at least one input");
   TQ_CHECK_ARG(n_steps == n_inputs - 1, "a pairwise path has n_inputs - 1 steps");
   TQ_CHECK_ARG(out_rank >= 0 && out_rank <= TQ_MAX_RANK, "output rank");
   TQ_CHECK_ARG(n_sliced >= 0 && n_sliced <= 62, "n_sliced");
   P = Plan{};
   P.dtype = dtype;
-  Compiler c(P);
+  Compiler c(P, 1, group_hint);
   TQ_TRY(c.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
                path, n_sliced, sliced_modes));
   if (P.lanes > 1) {
@@ -2548,12 +2553,44 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
     // a batch share their launches); kept if the second plan runs with the same lanes
     Plan Q{};
     Q.dtype = dtype;
-    Compiler c2(Q, P.lanes);
+    Compiler c2(Q, P.lanes, group_hint);
     if (c2.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
                path, n_sliced, sliced_modes) == TQ_OK && Q.lanes == P.lanes)
       P = std::move(Q);
   }
   plan_planes_layout(P);   // sizes known at compile time (queries, CPU tests); allocated at materialize
+  // the compile arguments, kept for a recompile with another group hint (plan_recompile)
+  CompileArgs& a = P.args;
+  int nm = 0;
+  for (int i = 0; i < n_inputs; ++i) nm += in_ranks[i];
+  a.in_ranks.assign(in_ranks, in_ranks + n_inputs);
+  a.in_modes.assign(in_modes, in_modes + nm);
+  a.in_extents.assign(in_extents, in_extents + nm);
+  a.in_strides.clear();
+  if (in_strides) a.in_strides.assign(in_strides, in_strides + nm);
+  a.out_modes.assign(out_modes, out_modes + out_rank);
+  a.path.assign(path, path + 2 * n_steps);
+  a.sliced.assign(sliced_modes, sliced_modes + n_sliced);
+  P.group_hint = group_hint;
+  return TQ_OK;
+}
+
+int plan_recompile(Plan& P, int group_hint) {
+  TQ_CHECK_ARG(P.d_arena == nullptr && P.d_tables == nullptr, "a plan is recompiled before its first execute only");
+  TQ_CHECK_ARG(!P.args.in_ranks.empty(), "plan has no compile arguments");
+  if (group_hint == P.group_hint) return TQ_OK;
+  const CompileArgs a = P.args;
+  const bool seq = P.use_seq, coop = P.use_coop, planes = P.use_planes, graph = P.use_graph;
+  Plan Q;
+  TQ_TRY(plan_compile(Q, P.dtype, (int)a.in_ranks.size(), a.in_ranks.data(), a.in_modes.data(),
+                      a.in_extents.data(), a.in_strides.empty() ? nullptr : a.in_strides.data(),
+                      (int)a.out_modes.size(), a.out_modes.data(), (int)a.path.size() / 2, a.path.data(),
+                      (int)a.sliced.size(), a.sliced.data(), group_hint));
+  Q.use_seq = seq;
+  Q.use_coop = coop;
+  Q.use_planes = planes;
+  Q.use_graph = graph;
+  P = std::move(Q);
   return TQ_OK;
 }
 
@@ -2570,6 +2607,8 @@ void plan_clone_compiled(const Plan& src, Plan& dst) {
   dst.graphs.clear();
   dst.graph_clock = 0;
   dst.cap_stream = nullptr;
+  dst.side_streams.clear();
+  dst.side_events.clear();
   dst.graph_builds = dst.graph_launches = 0;
   dst.ps_fallbacks = 0;
   dst.run_mode = 0;
@@ -2710,6 +2749,16 @@ int plan_release(Plan& P) {
   };
   drop_events(P.ev_used);
   drop_events(P.ev_free);
+  {
+    std::vector<hipStream_t> ks;
+    for (auto s : P.side_streams)
+      if (!rel(hipStreamDestroy(s), "group side stream", rc)) ks.push_back(s);
+    P.side_streams.swap(ks);
+    std::vector<hipEvent_t> ke;
+    for (auto e : P.side_events)
+      if (!rel(hipEventDestroy(e), "group event", rc)) ke.push_back(e);
+    P.side_events.swap(ke);
+  }
   if (P.owns_device) {
     if (P.d_arena && rel(hipFree(P.d_arena), "arena", rc)) P.d_arena = nullptr;
     if (P.d_tables && rel(hipFree(P.d_tables), "tables", rc)) P.d_tables = nullptr;
@@ -2959,13 +3008,56 @@ class Exec {
 
   int launch_one(Inst& x, const Op& op);
   int fill_s2(const Inst& x, S2Op& o, const Op& op, int stab) const;
+  // per-instance work of a group: member k > 0 on side stream k - 1 (forked from and joined back
+  // into the execution stream: parallel branches of the captured graph), member 0 on the stream
+  hipStream_t ost_ = nullptr;   // the stream launch_one / lane sums use (st_ unless forked)
+  template <typename F>
+  int each_instance(F&& f);
   int launch_chain(int b, int e, int coop);
   int launch(const std::vector<int>& grp);
 };
 
+template <typename F>
+int Exec::each_instance(F&& f) {
+  static const bool fork = [] {
+    const char* e = getenv("TQ_GROUP_FORK");
+    return !(e && e[0] == '0');
+  }();
+  const int n = (int)I_.size();
+  if (n == 1 || !fork) {
+    ost_ = st_;
+    for (auto& x : I_) TQ_TRY(f(x));
+    return TQ_OK;
+  }
+  Plan& P = P0_;
+  while ((int)P.side_streams.size() < n - 1) {
+    hipStream_t s = nullptr;
+    TQ_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    P.side_streams.push_back(s);
+  }
+  while ((int)P.side_events.size() < n) {
+    hipEvent_t e = nullptr;
+    TQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    P.side_events.push_back(e);
+  }
+  TQ_HIP(hipEventRecord(P.side_events[0], st_));
+  int rc = TQ_OK;
+  for (int k = 1; k < n && rc == TQ_OK; ++k) {
+    hipStream_t s = P.side_streams[k - 1];
+    TQ_HIP(hipStreamWaitEvent(s, P.side_events[0], 0));
+    ost_ = s;
+    rc = f(I_[k]);
+    TQ_HIP(hipEventRecord(P.side_events[k], s));
+  }
+  ost_ = st_;
+  if (rc == TQ_OK) rc = f(I_[0]);
+  for (int k = 1; k < n; ++k) TQ_HIP(hipStreamWaitEvent(st_, P.side_events[k], 0));
+  return rc;
+}
+
 int Exec::launch_one(Inst& x, const Op& op) {
   Plan& P = *x.P;
-  const hipStream_t st = st_;
+  const hipStream_t st = ost_ ? ost_ : st_;
   const double beta = op.writes_output ? x.beta_out : 0.0;
   const bool planes_on = planes_active(P);
   if (planes_on && op.kind == OP_GEMM && &op == &P.ops[P.planes_gemm]) {
@@ -3316,7 +3408,7 @@ int Exec::launch(const std::vector<int>& grp) {
     }
     for (size_t k = 0; k < I_.size(); ++k) set_lane(I_[k], keep[k]);
   } else {
-    for (auto& x : I_) TQ_TRY(launch_one(x, x.P->ops[grp[0]]));
+    TQ_TRY(each_instance([&](Inst& x) -> int { return launch_one(x, x.P->ops[grp[0]]); }));
   }
   if (prof) {
     TQ_HIP(hipEventRecord(ev.b, st_));
@@ -3401,29 +3493,32 @@ int Exec::run(int64_t s_begin, int64_t s_end, int64_t s_step, int accumulate) {
       if (merged || nl == 1) {
         set_lane_all(0);
         TQ_TRY(launch(grp));
-        if (merged && nl > 1)
-          for (auto& x : I_)
+        bool sums = false;
+        for (int j : grp) sums = sums || P0_.ops[j].lane_sum;
+        if (merged && nl > 1 && sums)
+          TQ_TRY(each_instance([&](Inst& x) -> int {
             for (int j : grp)
               if (x.P->ops[j].lane_sum) {   // a lane-merged level whose lanes an output permute sums
                 TQ_TRY(lane_sum_launch(x.P->dtype, x.P->ops[j].nc, ptr(x, x.P->ops[j].c),
-                                       (int64_t)(x.P->lane_stride / esz()), nl, st_));
+                                       (int64_t)(x.P->lane_stride / esz()), nl, ost_));
                 x.lanes_summed = true;
               }
+            return TQ_OK;
+          }));
       } else if (op0.kind == OP_GEMM && op0.lane_batch) {
         set_lane_all(0);
         lane_gemm_ = nl;
-        int rc = TQ_OK;
-        for (auto& x : I_) {
-          rc = launch_one(x, x.P->ops[grp[0]]);
-          if (rc != TQ_OK) break;
+        const int rc = each_instance([&](Inst& x) -> int {
+          TQ_TRY(launch_one(x, x.P->ops[grp[0]]));
           if (op0.lane_sum) {
             // (the pre-split GEMM's combine has summed the lanes already)
             if (!(planes_active(*x.P) && grp[0] == x.P->planes_gemm))
-              rc = lane_sum_launch(x.P->dtype, op0.nc, ptr(x, op0.c), (int64_t)(x.P->lane_stride / esz()), nl, st_);
+              TQ_TRY(lane_sum_launch(x.P->dtype, op0.nc, ptr(x, op0.c), (int64_t)(x.P->lane_stride / esz()), nl,
+                                     ost_));
             x.lanes_summed = true;
-            if (rc != TQ_OK) break;
           }
-        }
+          return TQ_OK;
+        });
         lane_gemm_ = 1;
         TQ_TRY(rc);
       } else if (op0.lane_once && I_[0].lanes_summed) {

@@ -113,8 +113,16 @@ struct InputView {
   std::vector<int64_t> slice_stride;  // per sliced mode (0 if absent)
 };
 
+// the arguments a plan was compiled from (kept for plan_recompile)
+struct CompileArgs {
+  std::vector<int32_t> in_ranks, in_modes, out_modes, path, sliced;
+  std::vector<int64_t> in_extents, in_strides;
+};
+
 struct Plan {
   int dtype = TQ_C64;
+  CompileArgs args;
+  int group_hint = 1;       // compiled for lockstep groups of this many plans (wider sweep chunks)
   size_t esz = 8;
   int n_inputs = 0;
   std::vector<InputView> inputs;
@@ -229,13 +237,18 @@ struct Plan {
   std::vector<GraphEntry> graphs;
   uint64_t graph_clock = 0;
   hipStream_t cap_stream = nullptr;
+  // a group execute led by this plan: side streams / events of its per-member branches
+  std::vector<hipStream_t> side_streams;
+  std::vector<hipEvent_t> side_events;
   int64_t graph_builds = 0, graph_launches = 0;
 };
 
 int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, const int32_t* in_modes,
                  const int64_t* in_extents, const int64_t* in_strides, int out_rank,
                  const int32_t* out_modes, int n_steps, const int32_t* path, int n_sliced,
-                 const int32_t* sliced_modes);
+                 const int32_t* sliced_modes, int group_hint = 1);
+// compile the plan again for lockstep groups of `group_hint` plans (before its first execute)
+int plan_recompile(Plan& P, int group_hint);
 // a copy of a compiled plan without any device state (arena, tables, graphs, events): the
 // same schedule for another stream / block (tq_plan_clone)
 void plan_clone_compiled(const Plan& src, Plan& dst);

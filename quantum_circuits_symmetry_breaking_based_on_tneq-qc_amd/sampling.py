@@ -77,6 +77,9 @@ class BlockPipeline:
         # the cores and input vectors are read-only: every member reads the same device copies
         base_ops = [torch.from_numpy(o).to(self.device, dtype) for o in task.operands]
         self.expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
+        if self.group > 1:
+            # compiled for lockstep groups: wider sweep chunks (G ops share every launch)
+            self.expr.plan(dtype, None, self.device.index).set("group_hint", self.group)
         self.slots: List[_Slot] = []
         for s in range(self.inflight):
             stream = torch.cuda.current_stream(self.device) if s == 0 else torch.cuda.Stream(self.device)

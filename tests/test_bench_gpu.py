@@ -21,12 +21,20 @@ COMMON = ["--config", "C4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"
 
 
 def _run(args, out):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + COMMON + ["--save-out", out],
+    """bench.py's stdout is ONE compact headline line; the full result comes from --details."""
+    details = out + ".details.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args + COMMON
+                       + ["--save-out", out, "--details", details],
                        capture_output=True, text=True, timeout=280, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    return json.loads(lines[0])
+    head = json.loads(lines[0])
+    assert len(lines[0]) <= 2048 and r.stdout.rstrip().splitlines()[-1] == lines[0]
+    with open(details) as f:
+        full = json.load(f)
+    assert head["value"] == full["value"]
+    return full
 
 
 def _close(a, b):

@@ -429,3 +429,23 @@ def test_planes_gemm_workspace_covers_every_lane_batch(cfg):
     assert "exceed the workspace" in _lib.last_error()
     # and unsupported shapes are refused before any sizing
     assert L.tq_planes_gemm_check(M + 1, N, K, 1, lda, ldb, ws) != 0
+
+
+def test_group_hint_recompiles_with_wider_chunks():
+    """A plan compiled for lockstep groups (tq_plan_set "group_hint", BlockPipeline --group):
+    the same ops and schedule, sweep ops with fewer, wider chunks (G ops share each launch);
+    refused after the first execute; a clone keeps the hint."""
+    import torch
+    e, p = _plan(config_task("C4"))
+    d1 = p.describe()
+    n1 = p.query("n_kernels")
+    p.set("group_hint", 4)
+    assert p.query("group_hint") == 4 and p.query("n_kernels") == n1
+    d4 = p.describe()
+    chunks = lambda d: sum(int(x) for x in re.findall(r"chunks=(\d+)", d))
+    if chunks(d1):
+        assert chunks(d4) < chunks(d1)
+    q = p.clone()
+    assert q.query("group_hint") == 4 and q.query("n_kernels") == n1
+    p.set("group_hint", 1)
+    assert p.describe() == d1
