@@ -96,6 +96,49 @@ std::string modes_str(const std::vector<int>& m) {
   return o.str();
 }
 
+// A sweep2 op's descriptor blob: the S2Desc, then the host-built tables the kernel reads instead
+// of walking the descriptor in LDS (S2Op::lanes / cbase): per thread of the 512 its load / store
+// element's byte offset and LDS address (threads beyond a small chunk duplicate element tid % n,
+// as the kernel's own enumeration), and per chunk (when there are at most kS2MaxCbTab) the memory
+// base of its load / store elements.
+std::vector<char> s2_blob(const S2Desc& d0, size_t esz) {
+  S2Desc d = d0;
+  auto al16 = [](size_t b) { return (b + 15) / 16 * 16; };
+  const size_t off_l = al16(sizeof(S2Desc));
+  const size_t off_c = off_l + (size_t)(1 << kS2LogThreads) * 16;
+  const bool cb = d.nchunks >= 1 && d.nchunks <= kS2MaxCbTab;
+  d.aux_lanes = (int32_t)off_l;
+  d.aux_cb = cb ? (int32_t)off_c : 0;
+  std::vector<char> blob(off_c + (cb ? (size_t)d.nchunks * 16 : 0), 0);
+  std::memcpy(blob.data(), &d, sizeof(S2Desc));
+  const int nin = 1 << d.nld, nout = 1 << d.nst;
+  uint32_t* lt = reinterpret_cast<uint32_t*>(blob.data() + off_l);
+  for (int tid = 0; tid < (1 << kS2LogThreads); ++tid) {
+    const int ti = tid & (nin - 1), to = tid & (nout - 1);
+    int64_t ldm = 0, stm = 0;
+    int lda = 0, sta = 0;
+    for (int b = 0; b < kS2LogThreads; ++b) {
+      if (b < d.nld && ((ti >> b) & 1)) { ldm += d.ld_w[b]; lda ^= d.ld_a[b]; }
+      if (b < d.nst && ((to >> b) & 1)) { stm += d.st_w[b]; sta ^= d.st_a[b]; }
+    }
+    lt[4 * tid + 0] = (uint32_t)(ldm * (int64_t)esz);
+    lt[4 * tid + 1] = (uint32_t)(stm * (int64_t)esz);
+    lt[4 * tid + 2] = (uint32_t)lda;
+    lt[4 * tid + 3] = (uint32_t)sta;
+  }
+  if (cb) {
+    int64_t* ct = reinterpret_cast<int64_t*>(blob.data() + off_c);
+    for (int64_t ch = 0; ch < d.nchunks; ++ch) {
+      int64_t bi = 0, bo = 0;
+      for (int b = d.logC; b < d.colbits; ++b)
+        if ((ch >> (b - d.logC)) & 1) { bi += d.k.w_in[b]; bo += d.k.w_out[b]; }
+      ct[2 * ch] = bi;
+      ct[2 * ch + 1] = bo;
+    }
+  }
+  return blob;
+}
+
 class Compiler {
  public:
   // lanes_hint > 1: the plan will run its slices in batches of that many lanes, so a
@@ -2010,17 +2053,13 @@ class Compiler {
       op.sgates.push_back(sg);
       flops += (double)d.ncols * count_of(sh.W[j]) * sg.K * (cplx_ ? 8.0 : 2.0);
     }
-    std::vector<char> blob(sizeof(S2Desc));
-    std::memcpy(blob.data(), &d, sizeof(S2Desc));
     op.stab = (int)P_.stabs.size();
-    P_.stabs.push_back(std::move(blob));
+    P_.stabs.push_back(s2_blob(d, P_.esz));
     if (d.nchunks == 1) {
       op.stab1 = op.stab;
     } else if (d1) {
-      std::vector<char> b1(sizeof(S2Desc));
-      std::memcpy(b1.data(), d1, sizeof(S2Desc));
       op.stab1 = (int)P_.stabs.size();
-      P_.stabs.push_back(std::move(b1));
+      P_.stabs.push_back(s2_blob(*d1, P_.esz));
     }
     op.flops = flops;
     op.bytes = (double)(n0 + nq) * P_.esz;
@@ -3222,6 +3261,15 @@ int Exec::fill_s2(const Inst& x, S2Op& o, const Op& op, int stab) const {
   o.use_beta = o.beta != 0.0;
   o.amax = op.amax_word >= 0 ? amax_lane(x, op.amax_word, x.cur) : nullptr;
   o.split_sc = P.run_mode && op.ps_gemm >= 0 ? sc_word(x, op.amax_word) : nullptr;
+  // host-built lane / chunk-base tables behind the descriptor (TQ_S2_HOSTTAB=0: computed in the
+  // kernel, the r05 prologue)
+  static const bool host_tabs = [] {
+    const char* e = getenv("TQ_S2_HOSTTAB");
+    return !(e && e[0] == '0');
+  }();
+  const char* blob = (const char*)P.d_tables + P.stab_off[stab];
+  o.lanes = host_tabs && hd->aux_lanes ? reinterpret_cast<const uint4*>(blob + hd->aux_lanes) : nullptr;
+  o.cbase = host_tabs && hd->aux_cb ? reinterpret_cast<const int64_t*>(blob + hd->aux_cb) : nullptr;
   return TQ_OK;
 }
 

@@ -104,6 +104,9 @@ struct S2Desc {
   // swizzle, the chosen one (tq_plan.cpp s2_layout)
   float lds_model[2] = {};
   int32_t nsync = 0;             // passes preceded by a workgroup barrier (kS2PmSync)
+  // byte offsets (in the plan's descriptor blob) of the host-built lane / chunk-base tables
+  // (S2Op::lanes / cbase), 0 = none
+  int32_t aux_lanes = 0, aux_cb = 0;
   alignas(8) S2Gate gate[kS2MaxGates];
 };
 constexpr int kS2KeepOff = (int)offsetof(S2Desc, k);
@@ -144,7 +147,13 @@ struct S2Op {
   // ((h_re, h_im | l_re, l_im) in the element's 8 bytes; the consuming GEMM's SplitPre); amax
   // still tracks the unscaled values
   const int32_t* split_sc = nullptr;
+  // host-built tables behind the descriptor (tq_plan.cpp s2_blob; nullptr = computed in the
+  // kernel): per thread (byte offset of its load / store element, LDS address of both), and per
+  // chunk (memory base of its load / store elements) -- S2Desc::aux_lanes / aux_cb
+  const uint4* lanes = nullptr;
+  const int64_t* cbase = nullptr;
 };
+constexpr int kS2MaxCbTab = 4096;   // chunks with a host-built base table, at most
 
 // streams of a chain launch (S2Launch::seq), a workgroup each
 constexpr int kS2SeqMaxStreams = 8;

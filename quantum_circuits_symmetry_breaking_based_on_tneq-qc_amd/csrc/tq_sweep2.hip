@@ -522,6 +522,20 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     continue;
   const S2Op& op = L.op[j];
   const S2Desc* __restrict__ d = op.desc;
+  // host-built per-thread lane offsets and per-chunk bases (S2Op::lanes / cbase, tq_plan.cpp
+  // s2_blob): loaded from memory together with the descriptor staging below -- no LDS table walk
+  // (and no barrier) between the descriptor and the first chunk's loads
+  const bool host_lanes = op.lanes != nullptr, host_cb = op.cbase != nullptr;
+  uint4 lane_e = {0u, 0u, 0u, 0u};
+  if (host_lanes) lane_e = op.lanes[tid];
+  int64_t hcb_in = 0, hcb_out = 0;
+  if (host_cb) {
+    const int64_t chl = ((int)blockIdx.x - op.block_begin) + (int64_t)(tid & 63) * op.nblocks;
+    if (chl < d->nchunks) {
+      hcb_in = op.cbase[2 * chl];
+      hcb_out = op.cbase[2 * chl + 1];
+    }
+  }
 #ifdef TQ_S2_TIMING
   const bool ts_rec = (int)blockIdx.x == op.block_begin;
   __shared__ unsigned int ts_slot;
@@ -619,7 +633,13 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   // beyond a small chunk duplicate element tid % n (same value to the same place)
   int64_t ldm = 0, stm = 0;
   int lda = 0, sta = 0;
-  {
+  constexpr int ESH = sizeof(T) == 4 ? 2 : sizeof(T) == 8 ? 3 : 4;
+  if (host_lanes) {
+    ldm = (int64_t)(lane_e.x >> ESH);
+    stm = (int64_t)(lane_e.y >> ESH);
+    lda = (int)lane_e.z;
+    sta = (int)lane_e.w;
+  } else {
     const int ti = tid & (nin - 1), to = tid & (nout - 1);
 #pragma unroll
     for (int b = 0; b < LOG_NT; ++b) {
@@ -647,8 +667,8 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   // with a lane read instead of a chain of dependent LDS reads per chunk.
   const int64_t nloc = (nchunks - lb + nb - 1) / nb;
   const bool lane_bases = nloc <= 64;
-  int64_t cb_in = 0, cb_out = 0;
-  {
+  int64_t cb_in = hcb_in, cb_out = hcb_out;
+  if (!host_cb) {
     const int64_t chl = lb + (int64_t)(tid & 63) * nb;
     for (int b0 = logC & ~7; b0 < colbits; b0 += 8) {   // batches of 8 weights in flight
       int64_t wi[8], wo[8];
@@ -673,8 +693,15 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), i);
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
   };
-  auto base_in = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_in, i) : chunk_base(ch, keep.w_in); };
-  auto base_out = [&](int i, int64_t ch) { return lane_bases ? lane64(cb_out, i) : chunk_base(ch, keep.w_out); };
+  // a chunk beyond the lanes' 64: from the host table through the scalar cache (a uniform read),
+  // else summed from the column-bit weights
+  using KI64 = const __attribute__((address_space(4))) int64_t*;
+  auto base_in = [&](int i, int64_t ch) {
+    return lane_bases ? lane64(cb_in, i) : host_cb ? ((KI64)op.cbase)[2 * ch] : chunk_base(ch, keep.w_in);
+  };
+  auto base_out = [&](int i, int64_t ch) {
+    return lane_bases ? lane64(cb_out, i) : host_cb ? ((KI64)op.cbase)[2 * ch + 1] : chunk_base(ch, keep.w_out);
+  };
   // The first chunk is loaded into RMAX register slots before the tables are staged (those
   // registers are free again before the gate passes).  Inside the chunk loop only chunks of at
   // most RPF slots are prefetched under the gate passes (the register-block passes need the

@@ -7,11 +7,12 @@ for spec in "$@"; do
   label=${spec%%:*}
   envs=${spec#*:}
   echo "== $label ($envs)"
-  env $envs timeout -k 10 200 python3 bench.py --config ${CFG:-C4} --no-cpu-baseline --no-c5 --no-alt --no-other --steps 20 > gpurun_out/abe_$label.log 2>&1 || exit 1
+  env $envs timeout -k 10 200 python3 bench.py --config ${CFG:-C4} --no-cpu-baseline --no-c5 --no-alt --no-other --steps ${STEPS:-40} > gpurun_out/abe_$label.log 2>&1 || exit 1
   python3 -c "
 import json
 d = json.loads([l for l in open('gpurun_out/abe_$label.log') if l.startswith('{')][-1])
-h = d.get('hbm_kernels') or {}
-print('$label', round(d['ms_per_step'], 4), 'ms/step', round(d['value'], 1), d['unit'], '| gemm/step',
-      h.get('gemm_ms_per_step'), 'sweep/step', h.get('sweep_ms_per_step'), 'sweep GB/s', h.get('sweep_GBps'))"
+r = d.get('roofline') or {}
+print('$label', round(d['ms_per_step'], 4), 'ms/step', round(d['value'], 1), d['unit'], '| latency',
+      (d.get('timing') or {}).get('latency_ms_per_step'), '| sweep avg us', r.get('avg_launch_us_events'),
+      'GB/s', r.get('achieved'))"
 done

@@ -3,7 +3,7 @@
 built with -DTQ_S2_TIMING (csrc: make BUILD=../lib/obj_timing OUT=../lib/libtneqhip_timing.so EXTRA=-DTQ_S2_TIMING): workgroup 0 of each op stamps the wall
 clock (100 MHz) at: start, descriptor staged, tables built, first chunk in LDS, first chunk's
 gates done, first chunk stored, end.  Prints per-op phase durations in us.
-    TNEQHIP_LIB=<timing build> python scripts/sweep_timing.py [C4|C3|C2] [slices]"""
+    TNEQHIP_LIB=<timing build> python scripts/sweep_timing.py [C4|C3|C2] [slices] [--group G]"""
 import ctypes, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -18,18 +18,35 @@ f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 f.restype = ctypes.c_int
 NREC, W = 2048, 48
 buf = (ctypes.c_ulonglong * (NREC * W))()
-task = config_task(sys.argv[1] if len(sys.argv) > 1 else "C4")
-expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
+import argparse
+ap = argparse.ArgumentParser()
+ap.add_argument("config", nargs="?", default="C4")
+ap.add_argument("slices", nargs="?", type=int, default=1)
+ap.add_argument("--group", type=int, default=1, help="time one lockstep group of G blocks (BlockPipeline)")
+args = ap.parse_args()
+task = config_task(args.config)
 dev = torch.device("cuda:0")
-ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
-out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
-SR = (0, int(sys.argv[2]) if len(sys.argv) > 2 else 1, 1)   # slices of the timed execute
+if args.group > 1:
+    from tneq_qc_amd.sampling import BlockPipeline
+    pipe = BlockPipeline(task, list(range(args.group)), inflight=1, group=args.group, device=dev)
+
+    def run():
+        for _ in range(args.group):
+            pipe.step()
+        pipe.synchronize()
+else:
+    expr = HipContractExpression(task.eq, *task.shapes, optimize=task.path, slices=task.sliced)
+    ops = [torch.from_numpy(o).to(dev, torch.complex64) for o in task.operands]
+    out = torch.empty(expr.out_shape, dtype=torch.complex64, device=dev)
+    SR = (0, args.slices, 1)   # slices of the timed execute
+
+    def run():
+        expr(*ops, out=out, slice_range=SR)
+        torch.cuda.synchronize()
 for _ in range(3):
-    expr(*ops, out=out, slice_range=SR)
-torch.cuda.synchronize()
+    run()
 f(buf, NREC)  # drain
-expr(*ops, out=out, slice_range=SR)
-torch.cuda.synchronize()
+run()
 n = f(buf, NREC)
 a = np.frombuffer(buf, dtype=np.uint64, count=n * W).reshape(n, W).astype(np.int64)
 a = a[np.argsort(a[:, 0])]
