@@ -88,6 +88,17 @@ extern "C" int tq_library_set(const char* key, int64_t value) {
 // development only (not in the public header): drains the sweep2 phase stamps of a library
 // built with -DTQ_S2_TIMING (9 x u64 per record); returns the record count (0 otherwise)
 extern "C" int tq_debug_sweep2_timing(unsigned long long* out, int n) { return tq::sweep2_timing(out, n); }
+// development only: in-kernel clock records of a -DTQ_KCLOCK build (tq_kclock.h), 4 x u64 each
+// (s_memtime, s_memrealtime at workgroup 0's start and end); which: 0 sweep2, 1 planes GEMM,
+// 2 the complex64 K-outer split GEMM.  Returns the record count (0 in the product build)
+extern "C" int tq_debug_kernel_clock(int which, unsigned long long* out, int n) {
+  switch (which) {
+    case 0: return tq::sweep2_kclock(out, n);
+    case 1: return tq::planes_gemm_kclock(out, n);
+    case 2: return tq::kouter_kclock(out, n);
+  }
+  return -1;
+}
 
 struct tq_plan_s {
   tq::Plan plan;

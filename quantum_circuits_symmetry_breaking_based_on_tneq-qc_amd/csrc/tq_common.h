@@ -199,6 +199,8 @@ struct PlanesCombineArgs {
 bool planes_gemm_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 int planes_gemm_splits(int64_t M, int64_t N, int64_t K, int64_t batch);
 size_t planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch);
+int planes_gemm_kclock(unsigned long long* out, int n);   // -DTQ_KCLOCK builds (tq_kclock.h)
+int kouter_kclock(unsigned long long* out, int n);
 int planes_gemm_check(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t lda, int64_t ldb, size_t ws_bytes);
 int planes_gemm_launch(const PlanesGemmArgs& a, const PlanesCombineArgs& c, hipStream_t stream);
 // y[i] = sum_{j < nl} y[i + j * stride] (elements), i < n: slice lanes summed into lane 0

@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "tq_common.h"
+#include "tq_kclock.h"
 
 namespace tq {
 
@@ -918,6 +919,7 @@ __global__ void __launch_bounds__(256) absmax_kouter_kernel(const float4* A, int
 }
 }  // namespace xbf
 
+TQ_KCLOCK_DEFINE(g_kclk_kouter)
 template <typename TL, typename SP>
 __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastArgs g) {
   using namespace xbf;
@@ -927,6 +929,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   constexpr int NGRP = TL::NGRP, NACC = G3 ? 3 : 2;
   static_assert(TL::NTERM == SP::NTERM, "tile / split terms");
   __shared__ __attribute__((aligned(16))) char lds[TL::SLOTS * BUF];
+  TQ_KCLOCK_BEGIN()
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid % WMW, wn = wid / WMW;
@@ -1448,6 +1451,7 @@ __global__ void __launch_bounds__(TL::NT, 1) gemm_c64_kouter_split_kernel(FastAr
   };
   if (beta != 0.f) store(std::true_type{});
   else store(std::false_type{});
+  TQ_KCLOCK_END(g_kclk_kouter)
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2503,6 +2507,8 @@ int skinny_strided_launch(int dtype, const SkinnyArgs& a, hipStream_t stream) {
     default: set_error("skinny: dtype"); return TQ_ERR_INVALID;
   }
 }
+
+int kouter_kclock(unsigned long long* out, int n) { return TQ_KCLOCK_READ(g_kclk_kouter, out, n); }
 
 size_t gemm_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t batch) {
   int64_t bm, bn, bk;

@@ -30,6 +30,7 @@
 #include <algorithm>
 
 #include "tq_common.h"
+#include "tq_kclock.h"
 
 namespace tq {
 
@@ -42,6 +43,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define TQ_LDS __attribute__((address_space(3)))
 
 constexpr int kBM = 256, kBN = 256, kBK = 32, kNT = 512;
+TQ_KCLOCK_DEFINE(g_kclk_gemmp)
 constexpr int kTB = kBK * kBM * 2;   // bytes of one plane tile (16 KiB)
 
 // chunk swizzle: the 32-byte chunk c of LDS row k holds global chunk c ^ f(k)
@@ -49,6 +51,7 @@ __device__ __forceinline__ int fsw(int k) { return (k & 3) | (((k >> 3) & 1) << 
 
 __global__ void __launch_bounds__(kNT) gemm_planes_kernel(PlanesGemmArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * 4 * kTB];
+  TQ_KCLOCK_BEGIN()
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
   // XCD-aware order (bijective for any count): the 8 round-robin XCD groups of workgroups
@@ -170,6 +173,7 @@ __global__ void __launch_bounds__(kNT) gemm_planes_kernel(PlanesGemmArgs g) {
         const int n = n0 + wn * 64 + j * 16 + (lane & 15);
         W[(int64_t)m * g.N + n] = acc[i][j][r];
       }
+  TQ_KCLOCK_END(g_kclk_gemmp)
 }
 
 // out(m, n) = sum over lanes j (lane_sum) or lane j alone of
@@ -251,6 +255,8 @@ size_t planes_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t batch) {
   for (int64_t b = 1; b <= batch; ++b) w = std::max(w, planes_ws_one(M, N, K, b));
   return w;
 }
+
+int planes_gemm_kclock(unsigned long long* out, int n) { return TQ_KCLOCK_READ(g_kclk_gemmp, out, n); }
 
 // the launcher's argument checks, host only (tq_planes_gemm_check: CPU tests of the sizing)
 int planes_gemm_check(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t lda, int64_t ldb, size_t ws_bytes) {

@@ -244,5 +244,6 @@ inline int s2d_blocks(int64_t ncols) {
 }
 int sweepd_launch(int dtype, const S2DLaunch& L, hipStream_t stream);
 int sweep2_timing(unsigned long long* out, int n);   // development instrumentation
+int sweep2_kclock(unsigned long long* out, int n);   // in-kernel clock records (-DTQ_KCLOCK builds)
 
 }  // namespace tq

@@ -32,10 +32,13 @@
 
 #include "tq_common.h"
 #include "tq_sweep2.h"
+#include "tq_kclock.h"
 
 namespace tq {
 
 namespace {
+
+TQ_KCLOCK_DEFINE(g_kclk_sweep2)
 
 constexpr int NT = 512, LOG_NT = 9;
 // the pass-barrier elision (kS2PmSync) assumes gi == threadIdx.x (mod NT) in gate_pass_u and
@@ -473,6 +476,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   const int32_t* const lut = &keep.lut[0][0];            // group -> LDS byte offset part
   const int tid = threadIdx.x;
   if (__builtin_amdgcn_wavefrontsize() != (1 << kS2WaveBits)) __builtin_trap();   // folded: wave64
+  TQ_KCLOCK_BEGIN()
   // ---- which op this workgroup works on: one op of a level (blockIdx ranges select it,
   // wave-uniform scan), or -- S2Launch::seq, one workgroup -- every op of a dependent chain in
   // order: op j + 1 reads what op j stored (same CU: its stores are complete before the next
@@ -979,6 +983,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
 #undef TQ_BY_COUNT
 #undef TQ_SLOTS
   }  // ops
+  TQ_KCLOCK_END(g_kclk_sweep2)
 }
 
 template <typename T>
@@ -1089,6 +1094,8 @@ int sweep2_timing(unsigned long long* out, int n) {
   return 0;
 #endif
 }
+
+int sweep2_kclock(unsigned long long* out, int n) { return TQ_KCLOCK_READ(g_kclk_sweep2, out, n); }
 
 int sweep2_launch(int dtype, const S2Launch& L, hipStream_t stream) {
   if (L.nops < 1 || L.nops > kS2MaxOps) {

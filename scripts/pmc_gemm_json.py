@@ -55,7 +55,7 @@ res = {
     "busy_cycles_per_mfma": c1["SQ_VALU_MFMA_BUSY_CYCLES"] / n_mfma,
     "avg_launch_ns_trace": avg_ns,
     "cycles_per_xcd": cyc_xcd,
-    "effective_clock_GHz": cyc_xcd / avg_ns,
+    "effective_clock_GHz": cyc_xcd / avg_ns if cyc_xcd / avg_ns <= 2.4 else None,   # null: unphysical (short dispatch)
     "mfma_busy_frac": c1["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc_xcd * 256 * 4),
     "FETCH_SIZE_kB_per_launch": c2.get("FETCH_SIZE"),
     "WRITE_SIZE_kB_per_launch": c3.get("WRITE_SIZE"),

@@ -50,7 +50,8 @@ res = {"config": "C4",
                   "--no-alt --steps 2 --warmup 1 (4 counter passes + a kernel-trace pass of the same command)",
        "definitions": {
            "hbm_bytes": "2*FETCH_SIZE + WRITE_SIZE (kB x 1024; gfx950 FETCH_SIZE correction)",
-           "effective_clock_GHz": "GRBM_GUI_ACTIVE / 8 XCDs / trace duration",
+           "effective_clock_GHz": "GRBM_GUI_ACTIVE / 8 XCDs / trace duration, null when > 2.4 GHz (unphysical for "
+                                  "short dispatches); the in-kernel clock: profiles/kclock_*.json",
            "mfma_busy_frac": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 256 CUs * 4 SIMDs)",
            "wait_frac": "SQ_WAIT_ANY / SQ_WAVE_CYCLES (share of resident wave cycles spent waiting)",
            "wait_lds_frac": "SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES"},
@@ -68,7 +69,10 @@ for key in sorted(trace, key=lambda k: (k[0], -len(trace[k]))):
     g = {"family": fam, "grid": grid, "dispatches": len(ns), "avg_ns": avg_ns, "counters_avg": c}
     if "GRBM_GUI_ACTIVE" in c and avg_ns > 0:
         cyc = c["GRBM_GUI_ACTIVE"] / 8
-        g["effective_clock_GHz"] = cyc / avg_ns
+        # GRBM_GUI_ACTIVE / 8 / duration is not a clock for short dispatches (r05: 2.8-10.8 GHz):
+        # kept only when physical (<= 2.4 GHz); the in-kernel clock is scripts/kernel_clock.py's
+        clk = cyc / avg_ns
+        g["effective_clock_GHz"] = clk if clk <= 2.4 else None
         g["mfma_busy_frac"] = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (cyc * 256 * 4)
     if c.get("SQ_WAVE_CYCLES"):
         g["wait_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
@@ -150,5 +154,5 @@ if os.path.exists(st):
     shutil.copy(st, f"profiles/rocprof_{TAG}_bench_kernel_stats.csv")
 for g in res["groups"]:
     print(g["family"], g["grid"], g["dispatches"], f"{g['avg_ns']/1e3:.1f}us",
-          {k: round(g[k], 3) for k in ("effective_clock_GHz", "mfma_busy_frac", "wait_frac", "wait_lds_frac")
+          {k: (round(g[k], 3) if g[k] is not None else None) for k in ("effective_clock_GHz", "mfma_busy_frac", "wait_frac", "wait_lds_frac")
            if g.get(k) is not None}, f"{g.get('hbm_GBps', 0):.0f} GB/s")

@@ -40,7 +40,7 @@ def _run(args, out):
 def _close(a, b):
     assert a.shape == b.shape == (2,) * 20
     err = np.abs(a - b).max() / np.abs(a).max()
-    assert err < 2e-5, err
+    assert err < 1e-5, err
 
 
 @pytest.mark.timeout(600)

@@ -9,9 +9,9 @@ seconds and through size-independent properties where it does not.
   2^16, C4g's on producer-split f16 planes with split-K.  Against the oracle's exact numpy
   contraction
   of the same sliced operands (oracle.contract_ref.sliced_operands, the slice enumeration of
-  tq_plan_execute).  Normwise bounds (relative to max|amp|): complex64 2e-5, complex128 1e-12.
+  tq_plan_execute).  Normwise bounds (relative to max|amp|): complex64 1e-5, complex128 1e-12.
   Componentwise (the Gauss-3M imaginary part): every amplitude with
-  |amp| >= 1e-2 max|amp| within 2e-3 relative, the normwise bound carried down to it.
+  |amp| >= 1e-2 max|amp| within 1e-3 relative, the normwise bound carried down to it.
 * C3 / C3d / C4 / C4g whole job EXACTLY as bench.py launches it (SlicedContraction at world 1
   over the full slice range: C4 8 slice lanes / C3 and C3d 32 / C4g 4, the f16-split boundary
   GEMM with operand-max words (C3 / C4g: lane-batched, per-lane words, lane_sum), lane-merged
@@ -21,7 +21,7 @@ seconds and through size-independent properties where it does not.
 * Lane skew: slices whose operands are 2^36 per cut leg larger than slice 0's, but whose
   contribution is exactly zero, batched in the same lanes as slice 0: the result must be slice
   0's amplitudes at full complex64 accuracy (a scale shared across lanes would flush them).
-* C3 / C4 / C3d / C4g whole job: sliced + hoisted execution equals the unsliced contraction (2e-5), every
+* C3 / C4 / C3d / C4g whole job: sliced + hoisted execution equals the unsliced contraction (1e-5), every
   4-way rank shard of the slices sums to the full result, and 0 < sum |amp|^2 <= 1 (the
   amplitudes are a sub-block of a unitary circuit's |psi>).
 """
@@ -30,7 +30,11 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"complex64": 2e-5, "complex128": 1e-12}
+# complex64: SURVEY.md §8(c)'s fp32 bound, 1e-5 of max|amp| (measured on the production launches,
+# profiles/accuracy_r06.json: 0.8e-6 .. 2.6e-6 normwise, as the oracle's own numpy complex64 run
+# of the same path: 0.9e-6 .. 1.2e-6); componentwise 100x that on |amp| >= 1e-2 max (measured
+# <= 1.7e-4, numpy complex64 7.7e-5)
+TOL = {"complex64": 1e-5, "complex128": 1e-12}
 
 
 def _expr_and_ops(task, dev, dtype, sliced=True):
