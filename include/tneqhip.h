@@ -168,7 +168,11 @@ int tq_plan_clone(tq_plan src, tq_plan* out);
  * (diagnostic: measured slower).  Its workgroups must be co-resident: a wait that gives up
  * (bounded spin) makes tq_plan_execute synchronize-check and fail with TQ_ERR_HIP ("the result
  * is invalid") instead of returning the stale result; inside a caller's capture the check is
- * skipped (query "coop_timeouts" then reports the count). */
+ * skipped (query "coop_timeouts" then reports the count).  Before the first execute only
+ * (the plan is compiled again): "group_hint" = G compiles for lockstep groups of G plans
+ * (tq_plan_execute_group: every sweep op shares its launches, so ops take G x fewer, wider
+ * chunks); "min_chunks" = n > 0 splits every big sweep op into at least n chunks (default 128,
+ * env TQ_S2_MINCHUNKS; a caller with several plans in flight on other streams wants fewer). */
 int tq_plan_set(tq_plan plan, const char* key, int64_t value);
 /* human-readable per-step description into buf (for debugging / DESIGN evidence) */
 int tq_plan_describe(tq_plan plan, char* buf, size_t n);

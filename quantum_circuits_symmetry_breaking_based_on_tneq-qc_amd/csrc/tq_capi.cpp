@@ -287,7 +287,16 @@ int tq_plan_set(tq_plan p, const char* key, int64_t value) {
       return TQ_ERR_INVALID;
     }
     TQ_GUARD_BEGIN
-    return tq::plan_recompile(p->plan, (int)value);
+    return tq::plan_recompile(p->plan, (int)value, p->plan.min_chunks);
+    TQ_GUARD_END
+  }
+  if (k == "min_chunks") {       // compile again: big sweep ops in at least `value` chunks (0: default)
+    if (p->materialized) {
+      tq::set_error("tq_plan_set: min_chunks before the plan's first execute only");
+      return TQ_ERR_INVALID;
+    }
+    TQ_GUARD_BEGIN
+    return tq::plan_recompile(p->plan, p->plan.group_hint, (int)value);
     TQ_GUARD_END
   }
   if (k == "sweep_coop") {       // 0: the multi-chunk sweep2 levels of a chain run one launch each
@@ -318,6 +327,7 @@ int64_t tq_plan_query(tq_plan p, const char* key) {
   if (k == "n_presplit") return P.n_ps;
   if (k == "lanes") return P.lanes;
   if (k == "group_hint") return P.group_hint;
+  if (k == "min_chunks") return P.min_chunks;
   if (k == "presplit_fallbacks") return P.ps_fallbacks;
   if (k == "n_gemm") return P.n_gemm;
   if (k == "n_apply") return P.n_apply;

@@ -145,8 +145,9 @@ class Compiler {
   // slice-dependent sweep op needs only min_chunks / lanes chunks to fill the GPU
   // group_hint > 1: the plan will run in lockstep groups of that many plans (blocks as lanes,
   // plan_run_group), so every sweep op shares its launches with group_hint - 1 others
-  Compiler(Plan& P, int lanes_hint = 1, int group_hint = 1)
-      : P_(P), lanes_hint_(lanes_hint), group_hint_(std::max(1, group_hint)) {}
+  // min_chunks > 0: the smallest chunk count of a big sweep op (else TQ_S2_MINCHUNKS / 128)
+  Compiler(Plan& P, int lanes_hint = 1, int group_hint = 1, int min_chunks = 0)
+      : P_(P), lanes_hint_(lanes_hint), group_hint_(std::max(1, group_hint)), min_chunks_(min_chunks) {}
 
   int run(int n_inputs, const int32_t* in_ranks, const int32_t* in_modes, const int64_t* in_ext,
           const int64_t* in_strides, int out_rank, const int32_t* out_modes, int n_steps,
@@ -1585,7 +1586,8 @@ class Compiler {
     lc = std::min(lc, d.colbits);
     // small tensors: narrower chunks, so that the op still spreads over >= s2_min_chunks()
     // workgroups (a 2^19-element tensor with a 256-element tile has only 64 chunks of 32 columns)
-    if (const int mc = std::max(1, s2_min_chunks() / (group_hint_ * ((c.dep && lanes_hint_ > 1) ? lanes_hint_ : 1)));
+    if (const int mc = std::max(1, (min_chunks_ > 0 ? min_chunks_ : s2_min_chunks()) /
+                                       (group_hint_ * ((c.dep && lanes_hint_ > 1) ? lanes_hint_ : 1)));
         mc > 1) {
       int lg = 0;
       while ((2 << lg) <= mc) ++lg;
@@ -2555,6 +2557,7 @@ class Compiler {
   Plan& P_;
   int lanes_hint_ = 1;
   int group_hint_ = 1;
+  int min_chunks_ = 0;
   bool one_chunk_ = false;   // s2_layout: one chunk of the whole tensor when it fits the tile
   bool cplx_ = false;
   int n_inputs_ = 0;
@@ -2575,16 +2578,17 @@ class Compiler {
 int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, const int32_t* in_modes,
                  const int64_t* in_extents, const int64_t* in_strides, int out_rank,
                  const int32_t* out_modes, int n_steps, const int32_t* path, int n_sliced,
-                 const int32_t* sliced_modes, int group_hint) {
+                 const int32_t* sliced_modes, int group_hint, int min_chunks) {
   TQ_CHECK_ARG(dtype_valid(dtype), "dtype");
   TQ_CHECK_ARG(group_hint >= 1, "group_hint");
+  TQ_CHECK_ARG(min_chunks >= 0, "min_chunks");
   TQ_CHECK_ARG(n_inputs >= 1, "need at least one input");
   TQ_CHECK_ARG(n_steps == n_inputs - 1, "a pairwise path has n_inputs - 1 steps");
   TQ_CHECK_ARG(out_rank >= 0 && out_rank <= TQ_MAX_RANK, "output rank");
   TQ_CHECK_ARG(n_sliced >= 0 && n_sliced <= 62, "n_sliced");
   P = Plan{};
   P.dtype = dtype;
-  Compiler c(P, 1, group_hint);
+  Compiler c(P, 1, group_hint, min_chunks);
   TQ_TRY(c.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
                path, n_sliced, sliced_modes));
   if (P.lanes > 1) {
@@ -2592,7 +2596,7 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
     // a batch share their launches); kept if the second plan runs with the same lanes
     Plan Q{};
     Q.dtype = dtype;
-    Compiler c2(Q, P.lanes, group_hint);
+    Compiler c2(Q, P.lanes, group_hint, min_chunks);
     if (c2.run(n_inputs, in_ranks, in_modes, in_extents, in_strides, out_rank, out_modes, n_steps,
                path, n_sliced, sliced_modes) == TQ_OK && Q.lanes == P.lanes)
       P = std::move(Q);
@@ -2611,20 +2615,21 @@ int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, cons
   a.path.assign(path, path + 2 * n_steps);
   a.sliced.assign(sliced_modes, sliced_modes + n_sliced);
   P.group_hint = group_hint;
+  P.min_chunks = min_chunks;
   return TQ_OK;
 }
 
-int plan_recompile(Plan& P, int group_hint) {
+int plan_recompile(Plan& P, int group_hint, int min_chunks) {
   TQ_CHECK_ARG(P.d_arena == nullptr && P.d_tables == nullptr, "a plan is recompiled before its first execute only");
   TQ_CHECK_ARG(!P.args.in_ranks.empty(), "plan has no compile arguments");
-  if (group_hint == P.group_hint) return TQ_OK;
+  if (group_hint == P.group_hint && min_chunks == P.min_chunks) return TQ_OK;
   const CompileArgs a = P.args;
   const bool seq = P.use_seq, coop = P.use_coop, planes = P.use_planes, graph = P.use_graph;
   Plan Q;
   TQ_TRY(plan_compile(Q, P.dtype, (int)a.in_ranks.size(), a.in_ranks.data(), a.in_modes.data(),
                       a.in_extents.data(), a.in_strides.empty() ? nullptr : a.in_strides.data(),
                       (int)a.out_modes.size(), a.out_modes.data(), (int)a.path.size() / 2, a.path.data(),
-                      (int)a.sliced.size(), a.sliced.data(), group_hint));
+                      (int)a.sliced.size(), a.sliced.data(), group_hint, min_chunks));
   Q.use_seq = seq;
   Q.use_coop = coop;
   Q.use_planes = planes;

@@ -123,6 +123,7 @@ struct Plan {
   int dtype = TQ_C64;
   CompileArgs args;
   int group_hint = 1;       // compiled for lockstep groups of this many plans (wider sweep chunks)
+  int min_chunks = 0;       // smallest chunk count of a big sweep op (0: TQ_S2_MINCHUNKS, default 128)
   size_t esz = 8;
   int n_inputs = 0;
   std::vector<InputView> inputs;
@@ -246,9 +247,10 @@ struct Plan {
 int plan_compile(Plan& P, int dtype, int n_inputs, const int32_t* in_ranks, const int32_t* in_modes,
                  const int64_t* in_extents, const int64_t* in_strides, int out_rank,
                  const int32_t* out_modes, int n_steps, const int32_t* path, int n_sliced,
-                 const int32_t* sliced_modes, int group_hint = 1);
-// compile the plan again for lockstep groups of `group_hint` plans (before its first execute)
-int plan_recompile(Plan& P, int group_hint);
+                 const int32_t* sliced_modes, int group_hint = 1, int min_chunks = 0);
+// compile the plan again for lockstep groups of `group_hint` plans and with `min_chunks` (0:
+// the default) chunks per big sweep op at least (before its first execute)
+int plan_recompile(Plan& P, int group_hint, int min_chunks);
 // a copy of a compiled plan without any device state (arena, tables, graphs, events): the
 // same schedule for another stream / block (tq_plan_clone)
 void plan_clone_compiled(const Plan& src, Plan& dst);
