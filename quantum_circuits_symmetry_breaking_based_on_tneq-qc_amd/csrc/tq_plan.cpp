@@ -2965,6 +2965,8 @@ int plan_launch(Plan& P, const void* const* inputs, void* out, int64_t s_begin, 
 // plan is exactly the single-plan executor.
 namespace {
 
+bool sweep_lanes_on();   // TQ_SWEEP_LANES (default 1): per-slice table sweeps lane-merged
+
 struct Inst {
   Plan* P = nullptr;
   const void* const* inputs = nullptr;
@@ -3052,6 +3054,8 @@ class Exec {
 
   int launch_one(Inst& x, const Op& op);
   int fill_s2(const Inst& x, S2Op& o, const Op& op, int stab) const;
+  SweepArgs sweep_args(const Inst& x, const Op& op, double beta) const;
+  int sweep_lanes_ = 0;   // > 0: the OP_SWEEP entry below runs every lane of the batch in one launch
   // per-instance work of a group: member k > 0 on side stream k - 1 (forked from and joined back
   // into the execution stream: parallel branches of the captured graph), member 0 on the stream
   hipStream_t ost_ = nullptr;   // the stream launch_one / lane sums use (st_ unless forked)
@@ -3060,6 +3064,63 @@ class Exec {
   int launch_chain(int b, int e, int coop);
   int launch(const std::vector<int>& grp);
 };
+
+// the table-driven sweep op's launch record for instance x's current lane
+SweepArgs Exec::sweep_args(const Inst& x, const Op& op, double beta) const {
+  const Plan& P = *x.P;
+      SweepArgs a;
+      const char* blob = (const char*)P.d_tables + P.stab_off[op.stab];
+      a.X = ptr(x, op.a);
+      a.Y = ptr(x, op.c);
+      a.ncols = op.ncols;
+      auto lg = [](int64_t v) {
+        if (v <= 0 || (v & (v - 1))) return -1;
+        int l = 0;
+        while ((int64_t(1) << l) < v) ++l;
+        return l;
+      };
+      a.nruns = op.nruns;
+      for (int r = 0; r < op.nruns; ++r) {
+        a.run_ext[r] = op.run_ext[r]; a.run_in[r] = op.run_in[r]; a.run_out[r] = op.run_out[r];
+        a.run_shift[r] = lg(op.run_ext[r]);
+      }
+      a.tin = op.tin;
+      a.tout = op.tout;
+      a.tin_shift = lg(op.tin);
+      a.tout_shift = lg(op.tout);
+      a.tabs = (const int32_t*)(blob + op.tabs_at);
+      a.tab_len = op.tab_len;
+      a.tin_off = (const int64_t*)blob;
+      a.tout_off = (const int64_t*)(blob + op.tout_off_at);
+      a.ngates = (int)op.sgates.size();
+      for (int j = 0; j < a.ngates; ++j) {
+        const SweepGate& g = op.sgates[j];
+        a.G[j] = ptr(x, g.g);
+        a.gidx[j] = g.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[g.gtab]) : nullptr;
+        a.K[j] = g.K; a.N[j] = g.N; a.W[j] = g.W;
+        a.tab_at[j] = (int)g.tab_off;
+      }
+      // power-of-two outer extents: per-bit column-offset weights
+      {
+        bool p2 = true;
+        int nb = 0;
+        for (int r = 0; r < op.nruns && p2; ++r) {
+          const int l = lg(op.run_ext[r]);
+          if (l < 0 || nb + l > 48) { p2 = false; break; }
+          for (int b = 0; b < l; ++b) {
+            a.w_in[nb + b] = op.run_in[r] << b;
+            a.w_out[nb + b] = op.run_out[r] << b;
+          }
+          nb += l;
+        }
+        a.colbits = p2 ? nb : -1;
+      }
+      a.load_colfast = op.load_colfast;
+      a.store_colfast = op.store_colfast;
+      a.use_beta = beta != 0.0;
+      a.beta = beta;
+  return a;
+}
 
 template <typename F>
 int Exec::each_instance(F&& f) {
@@ -3184,57 +3245,7 @@ int Exec::launch_one(Inst& x, const Op& op) {
       TQ_TRY(axpy_launch(P.dtype, op.n, ptr(x, op.a), ptr(x, op.c), beta, st));
       break;
     case OP_SWEEP: {
-      SweepArgs a;
-      const char* blob = (const char*)P.d_tables + P.stab_off[op.stab];
-      a.X = ptr(x, op.a);
-      a.Y = ptr(x, op.c);
-      a.ncols = op.ncols;
-      auto lg = [](int64_t v) {
-        if (v <= 0 || (v & (v - 1))) return -1;
-        int l = 0;
-        while ((int64_t(1) << l) < v) ++l;
-        return l;
-      };
-      a.nruns = op.nruns;
-      for (int r = 0; r < op.nruns; ++r) {
-        a.run_ext[r] = op.run_ext[r]; a.run_in[r] = op.run_in[r]; a.run_out[r] = op.run_out[r];
-        a.run_shift[r] = lg(op.run_ext[r]);
-      }
-      a.tin = op.tin;
-      a.tout = op.tout;
-      a.tin_shift = lg(op.tin);
-      a.tout_shift = lg(op.tout);
-      a.tabs = (const int32_t*)(blob + op.tabs_at);
-      a.tab_len = op.tab_len;
-      a.tin_off = (const int64_t*)blob;
-      a.tout_off = (const int64_t*)(blob + op.tout_off_at);
-      a.ngates = (int)op.sgates.size();
-      for (int j = 0; j < a.ngates; ++j) {
-        const SweepGate& g = op.sgates[j];
-        a.G[j] = ptr(x, g.g);
-        a.gidx[j] = g.gtab >= 0 ? (const int32_t*)((char*)P.d_tables + P.gtab_off[g.gtab]) : nullptr;
-        a.K[j] = g.K; a.N[j] = g.N; a.W[j] = g.W;
-        a.tab_at[j] = (int)g.tab_off;
-      }
-      // power-of-two outer extents: per-bit column-offset weights
-      {
-        bool p2 = true;
-        int nb = 0;
-        for (int r = 0; r < op.nruns && p2; ++r) {
-          const int l = lg(op.run_ext[r]);
-          if (l < 0 || nb + l > 48) { p2 = false; break; }
-          for (int b = 0; b < l; ++b) {
-            a.w_in[nb + b] = op.run_in[r] << b;
-            a.w_out[nb + b] = op.run_out[r] << b;
-          }
-          nb += l;
-        }
-        a.colbits = p2 ? nb : -1;
-      }
-      a.load_colfast = op.load_colfast;
-      a.store_colfast = op.store_colfast;
-      a.use_beta = beta != 0.0;
-      a.beta = beta;
+      const SweepArgs a = sweep_args(x, op, beta);
       TQ_TRY(sweep_launch(P.dtype, a, st));
       break;
     }
@@ -3373,7 +3384,7 @@ int Exec::launch(const std::vector<int>& grp) {
     ev = ev_begin(pkind);
     // a lane-batched GEMM or a sweep level merged across the batch's lanes does every lane's
     // work; a group does every instance's
-    const int mult = (lanes_merge ? nl : lane_gemm_) * (int)I_.size();
+    const int mult = (lanes_merge ? nl : sweep_lanes_ > 1 ? sweep_lanes_ : lane_gemm_) * (int)I_.size();
     for (int j : grp) {
       ev.flops += P0_.ops[j].flops * mult;
       ev.bytes += P0_.ops[j].bytes * mult;
@@ -3460,6 +3471,24 @@ int Exec::launch(const std::vector<int>& grp) {
       TQ_TRY(sweep2_launch(P0_.dtype, L, st_));
     }
     for (size_t k = 0; k < I_.size(); ++k) set_lane(I_[k], keep[k]);
+  } else if (op0.kind == OP_SWEEP && sweep_lanes_ > 1) {
+    // the per-slice table sweep of every lane in one launch (grid.y = lane; SweepLanes)
+    TQ_TRY(each_instance([&](Inst& x) -> int {
+      const Op& op = x.P->ops[grp[0]];
+      const int keep = x.cur;
+      SweepLanes ls;
+      ls.n = sweep_lanes_;
+      for (int j = 0; j < sweep_lanes_; ++j) {
+        set_lane(x, j);
+        ls.X[j] = ptr(x, op.a);
+        ls.Y[j] = ptr(x, op.c);
+        for (size_t g = 0; g < op.sgates.size(); ++g) ls.G[j][g] = ptr(x, op.sgates[g].g);
+      }
+      set_lane(x, 0);
+      const SweepArgs a = sweep_args(x, op, 0.0);
+      set_lane(x, keep);
+      return sweep_launch_lanes(x.P->dtype, a, ls, ost_ ? ost_ : st_);
+    }));
   } else {
     TQ_TRY(each_instance([&](Inst& x) -> int { return launch_one(x, x.P->ops[grp[0]]); }));
   }
@@ -3577,6 +3606,14 @@ int Exec::run(int64_t s_begin, int64_t s_end, int64_t s_step, int accumulate) {
       } else if (op0.lane_once && I_[0].lanes_summed) {
         set_lane_all(0);
         TQ_TRY(launch(grp));
+      } else if (op0.kind == OP_SWEEP && grp.size() == 1 && !op0.writes_output && sweep_lanes_on() &&
+                 nl <= kSweepMaxLanes) {
+        // a per-slice table sweep whose lanes write their own copies: one launch for the batch
+        set_lane_all(0);
+        sweep_lanes_ = nl;
+        const int rc = launch(grp);
+        sweep_lanes_ = 0;
+        TQ_TRY(rc);
       } else {
         for (int j = 0; j < nl; ++j) {
           set_lane_all(j);
@@ -3587,6 +3624,14 @@ int Exec::run(int64_t s_begin, int64_t s_end, int64_t s_step, int accumulate) {
     for (auto& x : I_) x.first = false;
   }
   return TQ_OK;
+}
+
+bool sweep_lanes_on() {
+  static const bool v = [] {
+    const char* e = getenv("TQ_SWEEP_LANES");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 // the plans of a group are the same compiled network (identical op lists and schedules)

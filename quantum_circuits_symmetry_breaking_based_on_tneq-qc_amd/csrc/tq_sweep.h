@@ -45,6 +45,18 @@ struct SweepArgs {
   double beta = 0.0;
 };
 
+// the slice lanes of one per-slice op in ONE launch (grid.y = lane): lane j reads X[j] and the
+// gate tensors G[j][*] and writes Y[j]; every other field (tables, tile, column weights) is the
+// SweepArgs' own, shared by the lanes (the same op on each lane's copy of the arena)
+constexpr int kSweepMaxLanes = 32;
+struct SweepLanes {
+  int n = 0;
+  const void* X[kSweepMaxLanes] = {};
+  void* Y[kSweepMaxLanes] = {};
+  const void* G[kSweepMaxLanes][kSweepMaxGates] = {};
+};
+
 int sweep_launch(int dtype, const SweepArgs& a, hipStream_t stream);
+int sweep_launch_lanes(int dtype, const SweepArgs& a, const SweepLanes& l, hipStream_t stream);
 
 }  // namespace tq

@@ -77,7 +77,7 @@ __device__ __forceinline__ void gate_pass(const T* src, T* dst, const int32_t* t
 }
 
 template <typename T, int WMAX>
-__global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a) {
+__global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a, SweepLanes ls) {
   constexpr int RMAX = WMAX * COLS / kThreads;  // staged elements per thread
   __shared__ T buf[2][WMAX * LD];
   __shared__ T gs[kSweepMaxGates * kSweepMaxKN];
@@ -87,14 +87,16 @@ __global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const T* __restrict__ X = reinterpret_cast<const T*>(a.X);
-  T* __restrict__ Y = reinterpret_cast<T*>(a.Y);
+  // a lane-merged launch (SweepLanes): blockIdx.y selects the slice lane's tensors
+  const int ln = ls.n > 0 ? (int)blockIdx.y : -1;
+  const T* __restrict__ X = reinterpret_cast<const T*>(ln >= 0 ? ls.X[ln] : a.X);
+  T* __restrict__ Y = reinterpret_cast<T*>(ln >= 0 ? ls.Y[ln] : a.Y);
   const bool pow2 = a.colbits >= 0;
   // ---- prologue: every table load independent of the others (one latency, not one per gate)
   for (int idx = tid; idx < a.ngates * kSweepMaxKN; idx += kThreads) {
     const int j = idx / kSweepMaxKN, t = idx - j * kSweepMaxKN;
     if (t < a.K[j] * a.N[j]) {
-      const T* G = reinterpret_cast<const T*>(a.G[j]);
+      const T* G = reinterpret_cast<const T*>(ln >= 0 ? ls.G[ln][j] : a.G[j]);
       gs[idx] = G[a.gidx[j] ? a.gidx[j][t] : t];
     }
   }
@@ -191,7 +193,7 @@ __global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a) {
 }
 
 template <typename T>
-int sweep_t(const SweepArgs& a, hipStream_t stream) {
+int sweep_t(const SweepArgs& a, const SweepLanes& ls, hipStream_t stream) {
   constexpr int WMAX = sizeof(T) > 8 ? 32 : 64;
   if (a.tin > WMAX || a.tout > WMAX) {
     set_error("sweep: tile too large for dtype");
@@ -201,18 +203,20 @@ int sweep_t(const SweepArgs& a, hipStream_t stream) {
   // 16 waves per workgroup (one output element per wave and gate pass at a 64-element tile);
   // 2 workgroups per CU fit in LDS; >= 2 chunks per workgroup let the register prefetch overlap
   const int64_t cap = 256 * 2;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, nchunks >= 2 * cap ? cap : std::max<int64_t>(256, (nchunks + 1) / 2)));
-  hipLaunchKernelGGL((sweep_kernel<T, WMAX>), dim3((unsigned)blocks), dim3(kThreads), 0, stream, a);
+  int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, nchunks >= 2 * cap ? cap : std::max<int64_t>(256, (nchunks + 1) / 2)));
+  const int nl = std::max(1, ls.n);
+  if (nl > 1) blocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, (2 * cap + nl - 1) / nl));   // one round shared
+  hipLaunchKernelGGL((sweep_kernel<T, WMAX>), dim3((unsigned)blocks, (unsigned)nl), dim3(kThreads), 0, stream, a, ls);
   TQ_HIP(hipGetLastError());
   return TQ_OK;
 }
 
 }  // namespace
 
-int sweep_launch(int dtype, const SweepArgs& a, hipStream_t stream) {
+int sweep_launch_lanes(int dtype, const SweepArgs& a, const SweepLanes& l, hipStream_t stream) {
   if (a.ncols == 0) return TQ_OK;
   if (a.ngates < 1 || a.ngates > kSweepMaxGates || a.nruns > kSweepMaxRuns || a.colbits > 48 ||
-      a.tab_len > kSweepTabMax) {
+      a.tab_len > kSweepTabMax || l.n < 0 || l.n > kSweepMaxLanes) {
     set_error("sweep: unsupported chain shape");
     return TQ_ERR_UNSUPPORTED;
   }
@@ -222,13 +226,17 @@ int sweep_launch(int dtype, const SweepArgs& a, hipStream_t stream) {
       return TQ_ERR_UNSUPPORTED;
     }
   switch (dtype) {
-    case TQ_F32: return sweep_t<float>(a, stream);
-    case TQ_F64: return sweep_t<double>(a, stream);
-    case TQ_C64: return sweep_t<c64>(a, stream);
-    case TQ_C128: return sweep_t<c128>(a, stream);
+    case TQ_F32: return sweep_t<float>(a, l, stream);
+    case TQ_F64: return sweep_t<double>(a, l, stream);
+    case TQ_C64: return sweep_t<c64>(a, l, stream);
+    case TQ_C128: return sweep_t<c128>(a, l, stream);
   }
   set_error("sweep: bad dtype");
   return TQ_ERR_INVALID;
+}
+
+int sweep_launch(int dtype, const SweepArgs& a, hipStream_t stream) {
+  return sweep_launch_lanes(dtype, a, SweepLanes{}, stream);
 }
 
 }  // namespace tq
