@@ -3284,6 +3284,7 @@ int Exec::fill_s2(const Inst& x, S2Op& o, const Op& op, int stab) const {
     return !(e && e[0] == '0');
   }();
   const char* blob = (const char*)P.d_tables + P.stab_off[stab];
+  o.rows = host_tabs ? (hd->npass & 0xff) | (hd->ngates & 0xff) << 8 | (hd->colbits & 0xff) << 16 : 0;
   o.lanes = host_tabs && hd->aux_lanes ? reinterpret_cast<const uint4*>(blob + hd->aux_lanes) : nullptr;
   o.cbase = host_tabs && hd->aux_cb ? reinterpret_cast<const int64_t*>(blob + hd->aux_cb) : nullptr;
   return TQ_OK;

@@ -152,6 +152,10 @@ struct S2Op {
   // chunk (memory base of its load / store elements) -- S2Desc::aux_lanes / aux_cb
   const uint4* lanes = nullptr;
   const int64_t* cbase = nullptr;
+  // the descriptor rows in use (host-filled from it; 0 = stage every row): npass | ngates << 8 |
+  // colbits << 16 -- the prologue stages only the group-table / pass / gate rows and column
+  // weights the op reads (a 2-pass op stages ~2 KiB of the 7-KiB S2Keep)
+  int32_t rows = 0, pad_rows = 0;
 };
 constexpr int kS2MaxCbTab = 4096;   // chunks with a host-built base table, at most
 

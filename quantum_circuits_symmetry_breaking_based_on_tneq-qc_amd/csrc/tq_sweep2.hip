@@ -497,12 +497,30 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     const KArg ko = (KArg)&o;
     return gi < kS2MaxGates ? (int)((((KWord)ko->gnum)[gi >> 2] >> ((gi & 3) * 8)) & 0xff) : 0;
   };
+  // descriptor words an op reads (S2Op::rows): S2Keep's group tables / pass rows below npass,
+  // gate rows below ngates, column weights below colbits; everything else is always staged
+  auto word_used = [](int i, int rows) {
+    if (rows == 0) return true;
+    const int b = i * 8 - kS2KeepOff;   // byte offset inside S2Keep
+    const int np = rows & 0xff, ng = (rows >> 8) & 0xff, cb = (rows >> 16) & 0xff;
+    constexpr int oWi = (int)offsetof(S2Keep, w_in), oWo = (int)offsetof(S2Keep, w_out),
+                  oHa = (int)offsetof(S2Keep, ld_ha), oL = (int)offsetof(S2Keep, lut),
+                  oG = (int)offsetof(S2Keep, gmeta), oP = (int)offsetof(S2Keep, pmeta);
+    if (b < oWi) return true;
+    if (b < oWo) return (b - oWi) / 8 < cb;
+    if (b < oHa) return (b - oWo) / 8 < cb;
+    if (b < oL) return true;
+    if (b < oG) return (b - oL) / (64 * 4) < np;
+    if (b < oP) return (b - oG) / (16 * 4) < ng;
+    return (b - oP) / (16 * 4) < np;
+  };
   auto load_desc = [&](const S2Op& o, uint2 (&w)[kIt], Raw (&g)[kGt]) {
     const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(o.desc);
+    const int rows = ((KArg)&o)->rows;   // a kernel argument (scalar)
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
       const int i = tid + it * NT;
-      if (i < kDescWords2) w[it] = gd[i];
+      if (i < kDescWords2 && word_used(i, rows)) w[it] = gd[i];
     }
     // gate gi = (i / kS2GateRaw) is wave-uniform (kS2GateRaw = the wave size): its element count
     // and pointer come from the kernel argument through the scalar cache
