@@ -242,13 +242,13 @@ def test_planes_gemm_equals_split_kernel(dev):
     ref = _oracle_full("C4g")
     _check(on, ref, TOL["complex64"], "planes")
     _check(off, ref, TOL["complex64"], "split")
-    assert np.abs(on - off).max() / np.abs(ref).max() < TOL["complex64"]
+    assert np.abs(on - off).max() / np.abs(ref).max() < 2 * TOL["complex64"]   # two complex64 results
     assert np.array_equal(on, again)
     # partial lane batches (3 + 5 slices over 4-lane batches): a launch of fewer entries than lanes
     # may take more split-K partials than a full one (planes_gemm_workspace covers every size)
     p1 = e(*ops, slice_range=(0, 3, 1)).cpu().numpy()
     p2 = e(*ops, slice_range=(3, e.n_slices, 1)).cpu().numpy()
-    assert np.abs(p1 + p2 - on).max() / np.abs(ref).max() < TOL["complex64"]
+    assert np.abs(p1 + p2 - on).max() / np.abs(ref).max() < 2 * TOL["complex64"]
 
 
 @pytest.mark.parametrize("cfg,lanes", [("C3", 32), ("C4", 8), ("C3d", 32), ("C4g", 4)])
@@ -290,14 +290,16 @@ def test_sliced_equals_unsliced(dev, cfg):
     sliced = e(*ops)
     e0, _ = _expr_and_ops(t, dev, torch.complex64, sliced=False)
     full = e0(*ops)
+    # two complex64 results, each within TOL of the exact amplitudes (checked against the oracle
+    # above): their difference is bounded by 2 TOL (C4g's unsliced path runs ONE K = 2^19 GEMM)
     err = (sliced - full).abs().max().item() / full.abs().max().item()
-    assert err < TOL["complex64"], err
+    assert err < 2 * TOL["complex64"], err
     # 4-way shard of the slices accumulated == full sum
     acc = torch.zeros_like(full)
     for r in range(4):
         e(*ops, out=acc, slice_range=(r, e.n_slices, 4), accumulate=True)
     err2 = (acc - full).abs().max().item() / full.abs().max().item()
-    assert err2 < TOL["complex64"], err2
+    assert err2 < 2 * TOL["complex64"], err2
     p = (full.abs() ** 2).sum().item()
     assert 0.0 < p <= 1.0 + 1e-4
 
@@ -317,6 +319,6 @@ def test_c4x4_holds_the_c4_block(dev):
     assert [q for q in t4.open_qubits if q not in (16, 37)] == t.open_qubits
     sub = big[idx]
     assert sub.shape == ref.shape
-    assert np.abs(sub - ref).max() / np.abs(ref).max() < TOL["complex64"]
+    assert np.abs(sub - ref).max() / np.abs(ref).max() < 2 * TOL["complex64"]   # two complex64 results
     p = float((np.abs(big) ** 2).sum())
     assert 0.0 < p <= 1.0 + 1e-4
