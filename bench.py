@@ -99,6 +99,18 @@ def _rocprof_avg_ns(name: str, kernel: str):
         return None
 
 
+ROCPROF_STATS = "rocprof_r06_bench_kernel_stats.csv"   # rocprofv3 --kernel-trace --stats of the bench command
+
+
+def _kernel_clock():
+    """In-kernel clocks of the benchmarked kernels (scripts/kernel_clock.py, committed)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "kclock_r06.json")) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
 def _cgroup_cpu_max():
     """The cgroup v2 CPU quota of this process ("max 100000" = none), if readable."""
     try:
@@ -607,7 +619,8 @@ def main():
         exe_def = ("executed f16 MFMA flops per launch (3 real products (Gauss) x 3 term products = 18*M*N*K) / "
                    "avg launch time of the GEMM + combine")
     elif f16:
-        pmc_b = _profile_json("pmc_gemm_f16_r04g.json" if f16_g3 else "pmc_gemm_f16_r02.json", args.config)
+        pmc_b = (_profile_json("pmc_gemm_f16_r06.json", args.config) or _profile_json("pmc_gemm_f16_r04g.json", args.config)
+                 if f16_g3 else _profile_json("pmc_gemm_f16_r02.json", args.config))
         pmc_t = pmc_b
         kdesc = ("boundary GEMM (complex64 on v_mfma_f32_32x32x16_f16: every f32 operand scaled by a power of two "
                  "(operand max from its producer sweep) and split into 2 f16 terms, 3 term products kept, f32 "
@@ -629,7 +642,15 @@ def main():
                  + ("Gauss 3M: 3 real f32 MFMA GEMMs per complex GEMM" if g3m
                     else "4 real f32 MFMA GEMMs per complex GEMM") + ")")
         exe_def = "executed MFMA flops per launch (3M: 6*M*N*K, 4M: 8*M*N*K real) / avg launch time"
-    clk = (pmc_b or {}).get("effective_clock_GHz")
+    # the GEMM's clock: measured inside the kernel (s_memtime / s_memrealtime, scripts/kernel_clock.py,
+    # profiles/kclock_r06.json), not GRBM_GUI_ACTIVE / 8 / duration (unphysical for short dispatches)
+    kcl = _kernel_clock()
+    clk = None
+    if kcl:
+        kname = "gemm_planes_kernel" if planes else "gemm_c64_kouter_split_kernel"
+        for sect in kcl.values():
+            if isinstance(sect, dict) and isinstance(sect.get(kname), dict):
+                clk = sect[kname].get("clock_GHz_median")
     gemm_rp = None
     if planes and args.config == "C4g":
         # rocprofv3 average of the same launch (GEMM + combine) from the committed kernel stats of
@@ -688,7 +709,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved / peak,
             "achieved_definition": exe_def + " (HIP events on the GEMM's stream, eager pass)",
-            "effective_clock_GHz_pmc": clk,
+            "clock_GHz_in_kernel": clk,
             "frac_at_measured_clock": (achieved / (peak * clk / PEAK_CLOCK_GHZ)) if clk else None,
             "algorithmic_tflops": alg_rate,
             "algorithmic_definition": "complex-GEMM flops 8*M*N*K per launch / avg launch time",
@@ -760,19 +781,20 @@ def main():
             })
         # rocprofv3 kernel stats of the default bench command (scripts/prof_round.sh r05f): the
         # average sweep2 launch there, priced with this step's algorithmic bytes per launch
-        st = _rocprof_avg_ns("rocprof_r05f_bench_kernel_stats.csv", "sweep2_kernel") if args.config == "C4" else None
+        st = _rocprof_avg_ns(ROCPROF_STATS, "sweep2_kernel") if args.config == "C4" else None
         if st and sweep_["launches"]:
             per_launch = sweep_["bytes"] / sweep_["launches"]
             res["roofline"]["avg_launch_us_events"] = sweep_["ms"] / sweep_["launches"] * 1e3
             res["roofline"]["avg_launch_us_rocprof"] = st / 1e3
             res["roofline"]["achieved_rocprof"] = per_launch / (st / 1e9) / 1e9
             res["roofline"]["frac_rocprof"] = res["roofline"]["achieved_rocprof"] / PEAK_HBM_GBS
-            res["roofline"]["rocprof_source"] = "profiles/rocprof_r05f_bench_kernel_stats.csv (sweep2_kernel, all forms)"
-        src = f"pmc_{args.config.lower()}_r05.json"
-        pmc_s = _profile_json(src, args.config)
-        if not pmc_s:
-            src = f"pmc_{args.config.lower()}_r04.json"
+            res["roofline"]["rocprof_source"] = f"profiles/{ROCPROF_STATS} (sweep2_kernel, all forms)"
+        pmc_s = None
+        for tag in ("r06", "r05", "r04"):
+            src = f"pmc_{args.config.lower()}_{tag}.json"
             pmc_s = _profile_json(src, args.config)
+            if pmc_s:
+                break
         if pmc_s and pmc_s.get("sweep_dispatches"):
             # HBM bytes of the sweep launches (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC passes of
             # this command), per launch x this step's launches
@@ -781,6 +803,16 @@ def main():
             res["roofline"]["traffic_unit"] = "bytes per step (sweep launches)"
             res["roofline"]["traffic_vs_algorithmic"] = per * sweep_["launches"] / max(1.0, sweep_["bytes"])
             res["roofline"]["traffic_source"] = f"profiles/{src}"
+        # the concurrency-aware rate of the headline: the step's algorithmic sweep bytes over the
+        # measured time per step WITH the blocks in flight (several launches overlap: the
+        # per-launch `achieved` is the one-launch-at-a-time rate)
+        agg = sweep_["bytes"] / (dt / args.steps) / 1e9 if dt > 0 else 0.0
+        res["roofline"]["aggregate_GBps"] = agg
+        res["roofline"]["aggregate_frac"] = agg / PEAK_HBM_GBS
+        res["roofline"]["aggregate_definition"] = ("algorithmic sweep bytes per step / ms_per_step of the headline "
+                                                   "(blocks in flight overlap their launches)")
+        if kcl and isinstance(kcl.get("C4_headline_regime", {}).get("sweep2_kernel"), dict):
+            res["roofline"]["clock_GHz_in_kernel"] = kcl["C4_headline_regime"]["sweep2_kernel"].get("clock_GHz_median")
     if slices_strong:
         res["slices_strong"] = slices_strong
     if rank == 0:
