@@ -795,6 +795,13 @@ def main():
             pmc_s = _profile_json(src, args.config)
             if pmc_s:
                 break
+        if pmc_s and not pmc_s.get("sweep_dispatches") and pmc_s.get("groups"):
+            # a scripts/prof_round.sh summary: per launch shape, the average HBM bytes of a dispatch
+            g2 = [g for g in pmc_s["groups"] if g.get("family") == "sweep2" and g.get("hbm_bytes") is not None]
+            nd = sum(g["dispatches"] for g in g2)
+            if nd:
+                pmc_s = dict(pmc_s, sweep_dispatches=nd,
+                             sweep_hbm_bytes=sum(g["hbm_bytes"] * g["dispatches"] for g in g2))
         if pmc_s and pmc_s.get("sweep_dispatches"):
             # HBM bytes of the sweep launches (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC passes of
             # this command), per launch x this step's launches
