@@ -49,8 +49,13 @@ struct SweepArgs {
 // gate tensors G[j][*] and writes Y[j]; every other field (tables, tile, column weights) is the
 // SweepArgs' own, shared by the lanes (the same op on each lane's copy of the arena)
 constexpr int kSweepMaxLanes = 32;
+constexpr int kSweepFanKN = 16;
 struct SweepLanes {
   int n = 0;
+  // fan-out (set by sweep_launch_lanes when every lane reads the SAME X -- a slice-invariant input
+  // of a per-slice op -- and every gate has K*N <= kSweepFanKN): X's chunk is loaded once and every
+  // lane's gates run on it in turn (the per-lane grid re-read X once per lane)
+  int fan = 0;
   const void* X[kSweepMaxLanes] = {};
   void* Y[kSweepMaxLanes] = {};
   const void* G[kSweepMaxLanes][kSweepMaxGates] = {};

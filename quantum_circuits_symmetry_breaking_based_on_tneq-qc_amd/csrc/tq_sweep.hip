@@ -76,27 +76,32 @@ __device__ __forceinline__ void gate_pass(const T* src, T* dst, const int32_t* t
   }
 }
 
-template <typename T, int WMAX>
+template <typename T, int WMAX, bool FAN>
 __global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a, SweepLanes ls) {
   constexpr int RMAX = WMAX * COLS / kThreads;  // staged elements per thread
-  __shared__ T buf[2][WMAX * LD];
-  __shared__ T gs[kSweepMaxGates * kSweepMaxKN];
+  // FAN: a third buffer keeps the chunk's input for every lane; the lanes' coefficients are all
+  // staged once per workgroup (K*N <= kSweepFanKN each)
+  __shared__ T buf[FAN ? 3 : 2][WMAX * LD];
+  __shared__ T gs[FAN ? kSweepMaxLanes * kSweepMaxGates * kSweepFanKN : kSweepMaxGates * kSweepMaxKN];
   __shared__ int64_t tio[2 * WMAX];              // tin_off | tout_off
   __shared__ int64_t lo_in[COLS], lo_out[COLS];  // lane part of the column offsets
   __shared__ int32_t tabs[kSweepTabMax];         // gate tables: per output element K source rows, n
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // a lane-merged launch (SweepLanes): blockIdx.y selects the slice lane's tensors
-  const int ln = ls.n > 0 ? (int)blockIdx.y : -1;
-  const T* __restrict__ X = reinterpret_cast<const T*>(ln >= 0 ? ls.X[ln] : a.X);
-  T* __restrict__ Y = reinterpret_cast<T*>(ln >= 0 ? ls.Y[ln] : a.Y);
+  // a lane-merged launch (SweepLanes): blockIdx.y selects the slice lane's tensors (FAN: every
+  // lane in turn inside the workgroup, X shared)
+  const int ln = ls.n > 0 && !FAN ? (int)blockIdx.y : -1;
+  const T* __restrict__ X = reinterpret_cast<const T*>(ln >= 0 ? ls.X[ln] : FAN ? ls.X[0] : a.X);
   const bool pow2 = a.colbits >= 0;
+  constexpr int GS = FAN ? kSweepFanKN : kSweepMaxKN;   // coefficient slots per gate in gs
+  const int nlg = FAN ? ls.n : 1;                       // lanes whose coefficients are staged
   // ---- prologue: every table load independent of the others (one latency, not one per gate)
-  for (int idx = tid; idx < a.ngates * kSweepMaxKN; idx += kThreads) {
-    const int j = idx / kSweepMaxKN, t = idx - j * kSweepMaxKN;
+  for (int idx = tid; idx < nlg * a.ngates * GS; idx += kThreads) {
+    const int lj = idx / GS, t = idx - lj * GS;
+    const int l = lj / a.ngates, j = lj - l * a.ngates;
     if (t < a.K[j] * a.N[j]) {
-      const T* G = reinterpret_cast<const T*>(ln >= 0 ? ls.G[ln][j] : a.G[j]);
+      const T* G = reinterpret_cast<const T*>(FAN ? ls.G[l][j] : ln >= 0 ? ls.G[ln][j] : a.G[j]);
       gs[idx] = G[a.gidx[j] ? a.gidx[j][t] : t];
     }
   }
@@ -142,6 +147,7 @@ __global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a, SweepLanes
     }
   };
 
+  constexpr int IN = FAN ? 2 : 0;   // the buffer the chunk enters
   int64_t ch = blockIdx.x;
   if (ch < nchunks) prefetch(ch);
   for (; ch < nchunks; ch += gridDim.x) {
@@ -151,44 +157,48 @@ __global__ void __launch_bounds__(kThreads) sweep_kernel(SweepArgs a, SweepLanes
       if (idx < nin) {
         int t, c;
         tc(idx, lcf, a.tin, a.tin_shift, t, c);
-        buf[0][t * LD + c] = reg[r];
+        buf[IN][t * LD + c] = reg[r];
       }
     }
     __syncthreads();
     const int64_t nxt = ch + gridDim.x;
     if (nxt < nchunks) prefetch(nxt);  // in flight while the gates run
-    for (int j = 0; j < a.ngates; ++j) {
-      const T* src = buf[j & 1] + lane;
-      T* dst = buf[(j + 1) & 1] + lane;
-      const int K = a.K[j], N = a.N[j], W = a.W[j];
-      const int32_t* tab = tabs + a.tab_at[j];
-      const T* g = gs + j * kSweepMaxKN;
-      switch (K) {
-        case 1: gate_pass<1>(src, dst, tab, g, K, N, W, wave); break;
-        case 2: gate_pass<2>(src, dst, tab, g, K, N, W, wave); break;
-        case 4: gate_pass<4>(src, dst, tab, g, K, N, W, wave); break;
-        default: gate_pass<0>(src, dst, tab, g, K, N, W, wave); break;
-      }
-      __syncthreads();
-    }
-    const T* res = buf[a.ngates & 1];
-    const int64_t c0 = ch * COLS;
-    const int64_t hi = pow2 ? chunk_offset(a.w_out, a.colbits, ch) : 0;
-    for (int idx = tid; idx < nout; idx += kThreads) {
-      int t, c;
-      tc(idx, scf, a.tout, a.tout_shift, t, c);
-      if (c0 + c < a.ncols) {
-        T v = res[t * LD + c];
-        const int64_t co = pow2 ? hi + lo_out[c] : col_offset_generic(a, c0 + c, true);
-        T* p = Y + co + tio[WMAX + t];
-        if (a.use_beta) {
-          if constexpr (sizeof(typename Traits<T>::R) == 4) v = v + *p * (float)a.beta;
-          else v = v + *p * a.beta;
+    for (int l = 0; l < nlg; ++l) {
+      T* __restrict__ Y = reinterpret_cast<T*>(FAN ? ls.Y[l] : ln >= 0 ? ls.Y[ln] : a.Y);
+      for (int j = 0; j < a.ngates; ++j) {
+        // FAN: gate 0 reads the kept input, later gates ping-pong between buffers 0 and 1
+        const T* src = (FAN ? (j == 0 ? buf[2] : buf[(j - 1) & 1]) : buf[j & 1]) + lane;
+        T* dst = (FAN ? buf[j & 1] : buf[(j + 1) & 1]) + lane;
+        const int K = a.K[j], N = a.N[j], W = a.W[j];
+        const int32_t* tab = tabs + a.tab_at[j];
+        const T* g = gs + (FAN ? (l * a.ngates + j) * GS : j * GS);
+        switch (K) {
+          case 1: gate_pass<1>(src, dst, tab, g, K, N, W, wave); break;
+          case 2: gate_pass<2>(src, dst, tab, g, K, N, W, wave); break;
+          case 4: gate_pass<4>(src, dst, tab, g, K, N, W, wave); break;
+          default: gate_pass<0>(src, dst, tab, g, K, N, W, wave); break;
         }
-        *p = v;
+        __syncthreads();
       }
+      const T* res = FAN ? buf[(a.ngates - 1) & 1] : buf[a.ngates & 1];
+      const int64_t c0 = ch * COLS;
+      const int64_t hi = pow2 ? chunk_offset(a.w_out, a.colbits, ch) : 0;
+      for (int idx = tid; idx < nout; idx += kThreads) {
+        int t, c;
+        tc(idx, scf, a.tout, a.tout_shift, t, c);
+        if (c0 + c < a.ncols) {
+          T v = res[t * LD + c];
+          const int64_t co = pow2 ? hi + lo_out[c] : col_offset_generic(a, c0 + c, true);
+          T* p = Y + co + tio[WMAX + t];
+          if (a.use_beta) {
+            if constexpr (sizeof(typename Traits<T>::R) == 4) v = v + *p * (float)a.beta;
+            else v = v + *p * a.beta;
+          }
+          *p = v;
+        }
+      }
+      __syncthreads();  // res / the buffers are rewritten by the next lane or chunk
     }
-    __syncthreads();  // res / buf[0] are rewritten by the next chunk
   }
 }
 
@@ -205,16 +215,39 @@ int sweep_t(const SweepArgs& a, const SweepLanes& ls, hipStream_t stream) {
   const int64_t cap = 256 * 2;
   int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, nchunks >= 2 * cap ? cap : std::max<int64_t>(256, (nchunks + 1) / 2)));
   const int nl = std::max(1, ls.n);
+  if constexpr (sizeof(T) <= 8) {   // (complex128: three tile buffers + the lanes' coefficients exceed LDS)
+    if (ls.fan && nl > 1) {
+      // X read once per chunk, every lane's gates in turn (one workgroup per CU: 3 tile buffers)
+      const int64_t fb = std::max<int64_t>(1, std::min<int64_t>(nchunks, 256));
+      hipLaunchKernelGGL((sweep_kernel<T, WMAX, true>), dim3((unsigned)fb), dim3(kThreads), 0, stream, a, ls);
+      TQ_HIP(hipGetLastError());
+      return TQ_OK;
+    }
+  }
   if (nl > 1) blocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, (2 * cap + nl - 1) / nl));   // one round shared
-  hipLaunchKernelGGL((sweep_kernel<T, WMAX>), dim3((unsigned)blocks, (unsigned)nl), dim3(kThreads), 0, stream, a, ls);
+  hipLaunchKernelGGL((sweep_kernel<T, WMAX, false>), dim3((unsigned)blocks, (unsigned)nl), dim3(kThreads), 0, stream, a, ls);
   TQ_HIP(hipGetLastError());
   return TQ_OK;
 }
 
 }  // namespace
 
-int sweep_launch_lanes(int dtype, const SweepArgs& a, const SweepLanes& l, hipStream_t stream) {
+int sweep_launch_lanes(int dtype, const SweepArgs& a, const SweepLanes& l0, hipStream_t stream) {
   if (a.ncols == 0) return TQ_OK;
+  // fan-out when every lane reads the same X and every gate fits kSweepFanKN coefficients
+  // (TQ_SWEEP_FAN=0: the per-lane grid)
+  static const bool fan_on = [] {
+    const char* e = getenv("TQ_SWEEP_FAN");
+    return !(e && e[0] == '0');
+  }();
+  SweepLanes l = l0;
+  l.fan = 0;
+  if (fan_on && l.n > 1 && !a.use_beta && dtype != TQ_C128) {
+    bool same = true;
+    for (int j = 1; j < l.n; ++j) same = same && l.X[j] == l.X[0];
+    for (int j = 0; j < a.ngates; ++j) same = same && a.K[j] * a.N[j] <= kSweepFanKN;
+    l.fan = same ? 1 : 0;
+  }
   if (a.ngates < 1 || a.ngates > kSweepMaxGates || a.nruns > kSweepMaxRuns || a.colbits > 48 ||
       a.tab_len > kSweepTabMax || l.n < 0 || l.n > kSweepMaxLanes) {
     set_error("sweep: unsupported chain shape");
