@@ -279,14 +279,15 @@ def c5_train(with_cpu: bool = True, steps: int = 20, warmup: int = 5, port: int 
                            "achieved_definition": "algorithmic bytes of the step's plans (tq_plan bytes_moved) x "
                                                   "candidate-steps/s",
                            "traffic": None}
-        pm = _profile_json("pmc_c5_r05.json", "C5")
+        pm_src = "pmc_c5_r06.json" if _profile_json("pmc_c5_r06.json", "C5") else "pmc_c5_r05.json"
+        pm = _profile_json(pm_src, "C5")
         if pm and pm.get("hbm_bytes_per_candidate_step"):
             # HBM bytes per candidate-step (2*FETCH_SIZE + WRITE_SIZE over every kernel of a
             # c5_bench run / its SGDG dispatches; rocprofv3 PMC passes, scripts/pmc_traffic.sh)
             out["roofline"]["traffic"] = pm["hbm_bytes_per_candidate_step"]
             out["roofline"]["traffic_unit"] = "bytes per candidate-step"
             out["roofline"]["traffic_vs_algorithmic"] = pm["hbm_bytes_per_candidate_step"] / ab
-            out["roofline"]["traffic_source"] = "profiles/pmc_c5_r05.json"
+            out["roofline"]["traffic_source"] = f"profiles/{pm_src}"
     tr = _profile_json("c5_trace_r04.json", "C5")
     if tr:
         out["gpu_busy_frac"] = tr.get("gpu_busy_frac")
