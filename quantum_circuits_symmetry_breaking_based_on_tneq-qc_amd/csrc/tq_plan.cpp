@@ -1453,6 +1453,99 @@ class Compiler {
     return r;
   }
 
+  // TQ_S2_REORDER (default 1): commute a chain's square gates into fuller register blocks
+  static bool s2_reorder_on() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_REORDER");
+      return !(e && e[0] == '0');
+    }();
+    return v;
+  }
+
+  // Register blocks take CONSECUTIVE square gates whose positions fit B bits (s2_layout
+  // block_span).  A brick-wall chain lists a layer's gates before the next layer's, so the greedy
+  // run closes a block at every layer's edge: (0,1)(2,3) | (4,5)(6,7) | (1,2)(3,4) ...  Square gates
+  // on disjoint positions commute (a square gate's outputs take its inputs' positions), so within
+  // each maximal run of square gates the gates are re-listed block by block: a block starts at
+  // the first unscheduled gate and takes every later gate whose overlapping predecessors (in the
+  // chain's order) are already scheduled or in the block, while the block's positions fit B bits.
+  // The result is a linear extension of the overlap order: per amplitude the same products,
+  // summed in another order of commuting factors (the rounding differs, the value does not).
+  // Non-square gates (expanding / contracting the working set) stay where they are.  False if
+  // the order is unchanged.
+  bool s2_reorder_squares(const Chain& c, Chain& out, int B) {
+    const int ng = (int)c.gates.size();
+    if (ng < 3) return false;
+    auto nbits = [&](int m) { return ilog2(ext_[m]); };
+    std::map<std::pair<int, int>, int> slot;   // (mode, bit) -> slot: s2_layout's positions, relabelled
+    int next = 0;
+    for (int m : c.X0.modes) for (int i = 0; i < nbits(m); ++i) slot[{m, i}] = next++;
+    std::vector<std::vector<int>> sl(ng);
+    std::vector<char> sq(ng, 0);
+    for (int j = 0; j < ng; ++j) {
+      const auto& g = c.gates[j];
+      std::vector<int> freed;
+      for (auto it = g.d.korder.rbegin(); it != g.d.korder.rend(); ++it)
+        for (int i = 0; i < nbits(*it); ++i) {
+          auto f = slot.find({*it, i});
+          if (f == slot.end()) return false;
+          freed.push_back(f->second);
+          slot.erase(f);
+        }
+      size_t fi = 0, nout = 0;
+      sl[j] = freed;
+      for (auto it = g.d.nfree.rbegin(); it != g.d.nfree.rend(); ++it)
+        for (int i = 0; i < nbits(*it); ++i, ++nout) {
+          const int s = fi < freed.size() ? freed[fi++] : next++;
+          slot[{*it, i}] = s;
+          if (nout >= freed.size()) sl[j].push_back(s);
+        }
+      sq[j] = g.d.K == g.d.N && (g.d.K == 2 || g.d.K == 4) && nout == freed.size();
+    }
+    auto overlap = [&](int a, int b) {
+      for (int x : sl[a]) for (int y : sl[b]) if (x == y) return true;
+      return false;
+    };
+    std::vector<int> order;
+    std::vector<char> done(ng, 0), inblk(ng, 0);
+    for (int j = 0; j < ng;) {
+      if (!sq[j]) { order.push_back(j++); continue; }
+      int e = j;
+      while (e < ng && sq[e]) ++e;
+      std::vector<int> rem;
+      for (int q = j; q < e; ++q) rem.push_back(q);
+      while (!rem.empty()) {
+        std::vector<int> blk{rem[0]}, U = sl[rem[0]];
+        inblk[rem[0]] = 1;
+        for (size_t t = 1; t < rem.size() && (int)blk.size() < kS2BlkMaxGates; ++t) {
+          const int g = rem[t];
+          bool ready = true;
+          for (int h = j; h < g && ready; ++h) if (!done[h] && !inblk[h] && overlap(h, g)) ready = false;
+          if (!ready) continue;
+          std::vector<int> u2 = U;
+          for (int x : sl[g]) if (std::find(u2.begin(), u2.end(), x) == u2.end()) u2.push_back(x);
+          if ((int)u2.size() > B) continue;
+          U = u2;
+          blk.push_back(g);
+          inblk[g] = 1;
+        }
+        for (int g : blk) {
+          done[g] = 1;
+          inblk[g] = 0;
+          order.push_back(g);
+          rem.erase(std::find(rem.begin(), rem.end(), g));
+        }
+      }
+      j = e;
+    }
+    bool same = true;
+    for (int j = 0; j < ng; ++j) same = same && order[j] == j;
+    if (same) return false;
+    out = c;
+    for (int j = 0; j < ng; ++j) out.gates[j] = c.gates[order[j]];
+    return true;
+  }
+
   // Layout of an in-place butterfly sweep (tq_sweep2.hip): every mode bit of the working set
   // gets a tile position (input tile bits memory-fastest first; a gate's outputs reuse the
   // positions it frees), the columns are the untouched mode bits ordered by stride, and a
@@ -1962,6 +2055,22 @@ class Compiler {
         group_lut(live & ~bm, d.k.lut[j]);
         j = e;
       }
+      if (getenv("TQ_S2_DUMP") && out) {
+        fprintf(stderr, "s2 op: %d gates, %d passes, logC %d, used %d:", d.ngates, d.npass, d.logC, used);
+        for (int q = 0; q < d.npass; ++q) {
+          const int f = d.k.pmeta[q][kS2PmFirst];
+          const int n = d.k.pmeta[q][kS2PmB] ? (d.k.pmeta[q][kS2PmCount] & 0xff) : 1;
+          fprintf(stderr, " |");
+          for (int g = f; g < f + n; ++g) {
+            uint32_t m = 0;
+            for (int k = 0; k < d.gate[g].K; ++k) m |= (uint32_t)kdep[g][k];
+            for (int k = 0; k < d.gate[g].N; ++k) m |= (uint32_t)ndep[g][k];
+            fprintf(stderr, " %dx%d:", d.gate[g].K, d.gate[g].N);
+            for (int b = 0; b < 16; ++b) if ((m >> b) & 1) fprintf(stderr, "%d", b);
+          }
+        }
+        fprintf(stderr, "\n");
+      }
       // group tables by pass (row p = the table of pass p's first gate): the kernel reads a
       // pass's row without first reading which gate starts it
       for (int q = 0; q < d.npass; ++q) {
@@ -2038,7 +2147,9 @@ class Compiler {
     op.a = src;
     op.c = tgt;
     op.writes_output = direct;
-    op.step = c.gates.back().step;
+    int step0 = c.gates.front().step;   // a re-listed chain (s2_reorder_squares): first / last path step
+    op.step = step0;
+    for (auto& g : c.gates) step0 = std::min(step0, g.step), op.step = std::max(op.step, g.step);
     op.tin = (int)sh.tin_n;
     op.tout = (int)sh.tout_n;
     op.ncols = d.ncols;
@@ -2066,7 +2177,7 @@ class Compiler {
     op.flops = flops;
     op.bytes = (double)(n0 + nq) * P_.esz;
     std::ostringstream o;
-    o << "step " << c.gates.front().step << ".." << op.step << " SWEEP2 " << what << "gates=" << c.gates.size()
+    o << "step " << step0 << ".." << op.step << " SWEEP2 " << what << "gates=" << c.gates.size()
       << " tin=" << op.tin << " tout=" << op.tout << " cols=" << op.ncols << " C=" << (1 << d.logC)
       << " chunks=" << d.nchunks << (direct ? " ->OUT" : "") << " KxN=";
     for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
@@ -2169,6 +2280,18 @@ class Compiler {
       } else {
         S2Desc d;
         if (!s2_layout(c, sh0, c.out_modes, &d)) { set_error("internal: sweep2 layout"); return TQ_ERR_INVALID; }
+        // the square gates re-listed into fuller register blocks, when that saves passes
+        Chain cr;
+        if (s2_reorder_on() && d.npass > 1 && s2_reorder_squares(c, cr, 4)) {
+          ChainShape shr;
+          S2Desc dr;
+          if (chain_shape(cr, cr.out_modes, shr) && shr.s2 && shr.tin_n == sh0.tin_n && shr.tout_n == sh0.tout_n &&
+              s2_layout(cr, shr, cr.out_modes, &dr) && dr.npass < d.npass) {
+            c = cr;
+            sh0 = shr;
+            d = dr;
+          }
+        }
         // a small tensor split into chunks for parallelism: also its one-chunk form, which a
         // chain launch (one workgroup running consecutive dependent ops) uses
         S2Desc d1;
