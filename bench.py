@@ -372,7 +372,7 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group backend for N > 1 (nccl = RCCL over xGMI)")
     ap.add_argument("--save-out", default=None, help="rank 0 saves the last step's amplitudes (.npy)")
-    ap.add_argument("--steps", type=int, default=50)   # steady state with two blocks in flight (10: +10 % per step)
+    ap.add_argument("--steps", type=int, default=50)   # steady state with four blocks in flight (10: +10 % per step)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C3d", "C4g", "C4x4"],
                     help="C4g: C4 on the big-boundary-GEMM path (each half swept whole); "
