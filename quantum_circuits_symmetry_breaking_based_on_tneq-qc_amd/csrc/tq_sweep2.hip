@@ -462,8 +462,15 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
                                         typename std::conditional<sizeof(T) == 8, double, float>::type>::type;
   static_assert(sizeof(Raw) == sizeof(T), "raw slot word");
   static_assert(RMAX <= kS2MaxSlots, "register slots");
-  __shared__ T buf[1 << CB];
-  __shared__ T cf[kS2MaxGates * kCf];                    // gate coefficients, k*N+n
+  // the gate coefficients first: their LDS addresses fit the 16-bit immediate offset of a
+  // ds_read (behind the 64-KiB tile a gate's 8 coefficient reads took a v_mov + s_add each)
+  struct alignas(16) Lds {
+    T cf[kS2MaxGates * kCf];                             // gate coefficients, k*N+n
+    T buf[1 << CB];
+  };
+  __shared__ Lds lds_main;
+  T* const cf = lds_main.cf;
+  T* const buf = lds_main.buf;
   static_assert(sizeof(S2Keep) % 8 == 0, "kept-table copy granularity");
   __shared__ uint2 keep_raw[sizeof(S2Keep) / 8];          // S2Desc::k, staged once
   // chain launches (S2Launch::seq) with LDS hand-offs: the dynamic LDS holds the tensor an op
