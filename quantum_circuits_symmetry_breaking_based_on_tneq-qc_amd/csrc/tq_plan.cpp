@@ -1313,6 +1313,15 @@ class Compiler {
     }();
     return v;
   }
+  // TQ_S2_LANEBLK=1: register blocks of 6 positions over 4 lanes (lane blocks; off by default:
+  // 28 % fewer passes on C4's big sweep ops, the same time -- DESIGN.md §3.3)
+  static bool s2_lane_blocks() {
+    static const bool v = [] {
+      const char* e = getenv("TQ_S2_LANEBLK");
+      return e && atoi(e) != 0;
+    }();
+    return v;
+  }
   // TQ_S2_WAVELOCAL=0: a workgroup barrier between every two sweep2 passes
   static bool s2_wave_local() {
     static const bool v = [] {
@@ -1747,16 +1756,131 @@ class Compiler {
       *live_out = live;
       return e;
     };
+    // Lane blocks (TQ_S2_LANEBLK): a register block over 6 positions, 4 in a thread's registers
+    // and 2 on its lane bits 4 and 5 (group-index bits 4 and 5: the other 3 threads of the block
+    // are lanes l ^ 16, l ^ 32, l ^ 48 of the same wave).  A gate whose position sits on a lane
+    // bit first trades it with a register bit the gate does not use (a swap: v_permlane16 /
+    // 32_swap, 2 instructions per element pair and dword; the register position evicted is the
+    // one used again latest).  C4's light-cone staircases hold 3 gates in 4 positions and 5 in 6:
+    // about 40 % fewer LDS passes on its big sweep ops for ~0.3 swaps per gate (r06 model).
+    struct PPlan {
+      int first = 0, end = 0;          // gates [first, end)
+      bool block = false, lanes = false;
+      uint32_t bm = 0, mask = 0;       // block positions (plain: B of them; lane: the 4 start
+                                       // registers), group positions (pass mask)
+      int reg0[4] = {}, reg1[4] = {};  // lane block: register bits' positions at start / end
+      int ln0[2] = {}, ln1[2] = {};    // lane bits 4 / 5: positions at start / end
+      std::vector<std::array<int, 3>> ops;   // lane block: {gate, slot i, slot j (-1: 2x2)} or {-1, lane bit, slot}
+      std::vector<int> order;          // group-index bits (after the columns) -> position
+    };
+    const bool lane_ok = s2_lane_blocks() && blocks && B == 4 && d.logC <= 4;
+    auto ascending = [](uint32_t m) {
+      std::vector<int> v;
+      for (; m; m &= m - 1) v.push_back(__builtin_ctz(m));
+      return v;
+    };
+    auto lane_span = [&](int j, int ng, int e4, PPlan& lp) {
+      if (!lane_ok || !square(j)) return false;
+      const uint32_t live = d.gate[j].pass_mask | kmask_of(j);
+      int e = j + 1;
+      uint32_t u = kmask_of(j);
+      while (e < ng && e - j < kS2BlkMaxGates && square(e) && __builtin_popcount(u | kmask_of(e)) <= 6)
+        u |= kmask_of(e), ++e;
+      for (; e > e4 && e - j >= 2; --e) {
+        // positions in order of first use, then untouched live positions (they stay on the lanes)
+        std::vector<int> first_use;
+        for (int q = j; q < e; ++q)
+          for (int p : ascending(kmask_of(q)))
+            if (std::find(first_use.begin(), first_use.end(), p) == first_use.end()) first_use.push_back(p);
+        if (first_use.size() <= 4 || first_use.size() > 6) continue;
+        uint32_t padded = 0;
+        for (int p : first_use) padded |= 1u << p;
+        for (int p : ascending(live & ~padded)) {
+          if (first_use.size() >= 6) break;
+          first_use.push_back(p);
+          padded |= 1u << p;
+        }
+        if (first_use.size() != 6) return false;
+        const std::vector<int> oth = ascending(live & ~padded);
+        if ((int)oth.size() < 4 - d.logC) return false;
+        int reg[4], ln[2];
+        for (int b = 0; b < 4; ++b) reg[b] = first_use[b];
+        ln[0] = first_use[4];
+        ln[1] = first_use[5];
+        PPlan r;
+        r.first = j;
+        r.end = e;
+        r.block = r.lanes = true;
+        std::copy(reg, reg + 4, r.reg0);
+        std::copy(ln, ln + 2, r.ln0);
+        auto slot = [&](int p) {
+          for (int b = 0; b < 4; ++b) if (reg[b] == p) return b;
+          return -1;
+        };
+        for (int q = j; q < e; ++q) {
+          const std::vector<int> gp = ascending(kmask_of(q));
+          for (int p : gp) {
+            if (slot(p) >= 0) continue;
+            const int l = ln[0] == p ? 0 : 1;
+            // evict the register position (not this gate's) whose next use is latest
+            int best = -1, best_next = -1;
+            for (int b = 0; b < 4; ++b) {
+              if (std::find(gp.begin(), gp.end(), reg[b]) != gp.end()) continue;
+              int nx = 1 << 20;
+              for (int t = q + 1; t < e; ++t)
+                if ((kmask_of(t) >> reg[b]) & 1) { nx = t; break; }
+              if (nx > best_next) best_next = nx, best = b;
+            }
+            r.ops.push_back({-1, l, best});
+            std::swap(reg[best], ln[l]);
+          }
+          // index bit t of the gate <-> position of input k = 1 << t
+          const int i0 = slot(__builtin_ctz((uint32_t)kdep[q][1]));
+          const int j0 = d.gate[q].K == 4 ? slot(__builtin_ctz((uint32_t)kdep[q][2])) : -1;
+          r.ops.push_back({q, i0, j0});
+        }
+        if ((int)r.ops.size() > kS2BlkMaxGates) continue;
+        std::copy(reg, reg + 4, r.reg1);
+        std::copy(ln, ln + 2, r.ln1);
+        for (int b = 0; b < 4; ++b) r.bm |= 1u << r.reg0[b];
+        r.mask = live & ~r.bm;
+        // lane bits 4 / 5 are group-index bits 4 / 5: the lane positions at order 4 - logC, 5 - logC
+        r.order.assign(oth.begin(), oth.begin() + (4 - d.logC));
+        r.order.push_back(r.ln0[0]);
+        r.order.push_back(r.ln0[1]);
+        r.order.insert(r.order.end(), oth.begin() + (4 - d.logC), oth.end());
+        lp = r;
+        return true;
+      }
+      return false;
+    };
+    auto plan_passes = [&](int ng) {
+      std::vector<PPlan> v;
+      for (int j = 0; j < ng;) {
+        uint32_t bm = 0, lv = 0;
+        const int e = block_span(j, ng, &bm, &lv);
+        PPlan pp;
+        if (lane_span(j, ng, e, pp)) {
+          v.push_back(pp);
+          j = pp.end;
+          continue;
+        }
+        pp.first = j;
+        pp.end = e;
+        pp.block = e - j >= 2;
+        pp.bm = pp.block ? bm : 0;
+        pp.mask = pp.block ? (lv & ~bm) : d.gate[j].pass_mask;
+        pp.order = ascending(pp.mask);
+        v.push_back(pp);
+        j = e;
+      }
+      return v;
+    };
     // a last gate inside a register block costs no pass of its own: no epilogue then
     bool last_alone = true;
     {
-      const int ng = (int)c.gates.size();
-      uint32_t bm, lv;
-      for (int j = 0; j < ng;) {
-        const int e = block_span(j, ng, &bm, &lv);
-        if (e == ng) last_alone = e - j == 1;
-        j = e;
-      }
+      const std::vector<PPlan> pl = plan_passes((int)c.gates.size());
+      if (!pl.empty()) last_alone = pl.back().end - pl.back().first == 1;
     }
     d.epi = 0;
     if (s2_epi_enabled() && last_alone && !last_np.empty()) {
@@ -1832,18 +1956,15 @@ class Compiler {
       };
       pats.push_back({enum_dirs(ld), 0.0, double(int64_t(1) << d.nld)});
       pats.push_back({enum_dirs(st), double(int64_t(1) << d.nst), 0.0});
-      const int ng = (int)c.gates.size() - (d.epi ? 1 : 0);   // as the pass loop below
-      for (int j = 0; j < ng;) {
-        uint32_t bm, lv, mask;
+      // as the pass loop below (the lane bits of a lane block: its start layout)
+      for (const PPlan& pp : plan_passes((int)c.gates.size() - (d.epi ? 1 : 0))) {
         double rd, wr;
-        const int e = block_span(j, ng, &bm, &lv);
-        if (e - j < 2) mask = d.gate[j].pass_mask, rd = d.gate[j].K, wr = d.gate[j].N;
-        else mask = lv & ~bm, rd = wr = double(1 << B);
-        j = e - j < 2 ? j + 1 : e;
+        if (!pp.block) rd = d.gate[pp.first].K, wr = d.gate[pp.first].N;
+        else rd = wr = double(1 << B);
         std::vector<int> v;
         for (int q = 0; q < d.logC && v.size() < 5; ++q) v.push_back(-(q + 1));
-        for (uint32_t m = mask; m && v.size() < 5; m &= m - 1) v.push_back(__builtin_ctz(m));
-        const double groups = double(int64_t(1) << (d.logC + __builtin_popcount(mask)));
+        for (size_t t = 0; t < pp.order.size() && v.size() < 5; ++t) v.push_back(pp.order[t]);
+        const double groups = double(int64_t(1) << (d.logC + __builtin_popcount(pp.mask)));
         pats.push_back({v, groups * rd, groups * wr});
       }
       double ideal = 0;
@@ -1981,31 +2102,48 @@ class Compiler {
         d.k.lut[j][jj] = ((base << d.logC) ^ sw) * (int32_t)P_.esz;   // bytes
       }
     }
-    // passes: register blocks of consecutive square gates (S2Desc::pmeta), single gates otherwise
+    // passes: register blocks of consecutive square gates (S2Desc::pmeta) -- plain, or lane
+    // blocks (plan_passes) -- single gates otherwise
     {
       const int ng = (int)c.gates.size() - (d.epi ? 1 : 0);   // the epilogue gate is no pass
-      auto group_lut = [&](uint32_t pass_mask, int32_t* lut) {
+      // group table of a pass: group-index bits (after the columns) -> positions, in `order`
+      auto group_lut = [&](const std::vector<int>& order, int32_t* lut) {
         for (int jj = 0; jj < 64; ++jj) {
           const int half = jj >> 5, v = jj & 31;
-          uint32_t m = pass_mask;
           int base = 0, sw = 0;
-          for (int t = 0; m; ++t) {
-            const int lo = __builtin_ctz(m);
-            m &= m - 1;
+          for (int t = 0; t < (int)order.size(); ++t) {
+            const int lo = order[t];
             if (half == 0 && t < 5 && ((v >> t) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
             if (half == 1 && t >= 5 && ((v >> (t - 5)) & 1)) { base |= 1 << lo; sw ^= d.vsw[lo]; }
           }
           lut[jj] = ((base << d.logC) ^ sw) * (int32_t)P_.esz;   // bytes
         }
       };
-      int j = 0;
+      auto addr = [&](int pos) { return ((1 << pos) << d.logC) ^ d.vsw[pos]; };   // elements
+      // a gate's block code from its register slots; canonical placement I < J: swap the gate's
+      // two legs -- input / output index bits 0 and 1 of every coefficient (a square gate: its
+      // outputs sit on its inputs' positions).  The kernel then needs 6 (B = 4) / 3 (B = 3)
+      // block-gate bodies instead of 12 / 6 (instruction-cache footprint, tq_sweep2.hip blk_gate)
+      auto gate_code = [&](int q, int i0, int j0) {
+        if (d.gate[q].K != 4) return i0;
+        if (i0 > j0) {
+          uint8_t cg[16];
+          auto sw = [](int v) { return ((v & 1) << 1) | ((v >> 1) & 1); };
+          for (int k = 0; k < 4; ++k)
+            for (int n = 0; n < 4; ++n) cg[sw(k) * 4 + sw(n)] = d.cgidx[q][k * 4 + n];
+          for (int t = 0; t < 16; ++t) d.cgidx[q][t] = cg[t];
+          std::swap(i0, j0);
+        }
+        return i0 | (j0 << 2) | 16;
+      };
+      const std::vector<PPlan> plan = plan_passes(ng);
+      if ((int)plan.size() > kS2MaxGates) return false;
       d.npass = 0;
-      while (j < ng) {
+      for (const PPlan& pp : plan) {
+        const int j = pp.first;
         int32_t* pm = d.k.pmeta[d.npass++];
         pm[kS2PmFirst] = j;
-        uint32_t bm = 0, live = 0;
-        const int e = block_span(j, ng, &bm, &live);
-        if (e - j < 2) {
+        if (!pp.block) {
           // a single-gate pass carries the gate's fields itself (S2Keep::pmeta): the kernel
           // reads a pass's whole head in one batch, ahead of the pass
           const S2Gate& G = d.gate[j];
@@ -2014,59 +2152,62 @@ class Compiler {
           pm[kS2PmPass] = (int32_t)G.pass_mask;
           for (int k = 0; k < kS2MaxK; ++k) pm[kS2PmAddr + k] = k < G.K ? G.kaddr[k] : 0;
           for (int n = 0; n < kS2MaxKN; ++n) pm[kS2PmCode + n] = n < G.N ? G.naddr[n] : 0;
-          j += 1;
+          group_lut(pp.order, d.k.lut[j]);
           continue;
         }
-        pm[kS2PmCount] = e - j;
-        pm[kS2PmB] = B;
-        pm[kS2PmPass] = (int32_t)(live & ~bm);
-        int bp[4], nb = 0;
-        for (int q = 0; q < kS2MaxPos; ++q)
-          if ((bm >> q) & 1) bp[nb++] = q;
-        for (int b = 0; b < B; ++b)
-          pm[kS2PmAddr + b] = ((1 << bp[b]) << d.logC) ^ d.vsw[bp[b]];
-        auto local = [&](int pos) {
-          for (int b = 0; b < B; ++b) if (bp[b] == pos) return b;
-          return -1;
-        };
-        for (int q = j; q < e; ++q) {
-          const S2Gate& G = d.gate[q];
-          // index bit t of the gate <-> position of input k = 1 << t
-          int i0 = local(__builtin_ctz((uint32_t)kdep[q][1]));
-          int code = i0;
-          if (G.K == 4) {
-            int j0 = local(__builtin_ctz((uint32_t)kdep[q][2]));
-            if (i0 > j0) {
-              // canonical placement I < J: swap the gate's two legs -- input / output index bits
-              // 0 and 1 of every coefficient (a square gate: its outputs sit on its inputs'
-              // positions).  The kernel then needs 6 (B = 4) / 3 (B = 3) block-gate bodies
-              // instead of 12 / 6 (instruction-cache footprint, tq_sweep2.hip blk_gate)
-              uint8_t cg[16];
-              auto sw = [](int v) { return ((v & 1) << 1) | ((v >> 1) & 1); };
-              for (int k = 0; k < 4; ++k)
-                for (int n = 0; n < 4; ++n) cg[sw(k) * 4 + sw(n)] = d.cgidx[q][k * 4 + n];
-              for (int t = 0; t < 16; ++t) d.cgidx[q][t] = cg[t];
-              std::swap(i0, j0);
-            }
-            code = i0 | (j0 << 2) | 16;
+        pm[kS2PmPass] = (int32_t)pp.mask;
+        if (pp.lanes) {
+          pm[kS2PmCount] = (int)pp.ops.size();
+          pm[kS2PmB] = 4 | kS2PmLanes;
+          for (int b = 0; b < 4; ++b) {
+            pm[kS2PmAddr + b] = addr(pp.reg0[b]);
+            pm[kS2PmAddrEnd + b] = addr(pp.reg1[b]);
           }
-          pm[kS2PmCode + (q - j)] = code;
+          pm[kS2PmLaneDelta] = addr(pp.ln0[0]) ^ addr(pp.ln1[0]);
+          pm[kS2PmLaneDelta + 1] = addr(pp.ln0[1]) ^ addr(pp.ln1[1]);
+          for (size_t t = 0; t < pp.ops.size(); ++t) {
+            const auto& o = pp.ops[t];
+            pm[kS2PmCode + (int)t] = o[0] < 0 ? (kS2SwapCode | (o[1] << 2) | o[2]) : gate_code(o[0], o[1], o[2]);
+          }
+        } else {
+          pm[kS2PmCount] = pp.end - pp.first;
+          pm[kS2PmB] = B;
+          int bp[4], nb = 0;
+          for (int q = 0; q < kS2MaxPos; ++q)
+            if ((pp.bm >> q) & 1) bp[nb++] = q;
+          for (int b = 0; b < B; ++b) pm[kS2PmAddr + b] = pm[kS2PmAddrEnd + b] = addr(bp[b]);
+          pm[kS2PmLaneDelta] = pm[kS2PmLaneDelta + 1] = 0;
+          auto local = [&](int pos) {
+            for (int b = 0; b < B; ++b) if (bp[b] == pos) return b;
+            return -1;
+          };
+          for (int q = pp.first; q < pp.end; ++q) {
+            // index bit t of the gate <-> position of input k = 1 << t
+            const int i0 = local(__builtin_ctz((uint32_t)kdep[q][1]));
+            const int j0 = d.gate[q].K == 4 ? local(__builtin_ctz((uint32_t)kdep[q][2])) : -1;
+            pm[kS2PmCode + (q - pp.first)] = gate_code(q, i0, j0);
+          }
         }
-        group_lut(live & ~bm, d.k.lut[j]);
-        j = e;
+        group_lut(pp.order, d.k.lut[j]);
       }
       if (getenv("TQ_S2_DUMP") && out) {
         fprintf(stderr, "s2 op: %d gates, %d passes, logC %d, used %d:", d.ngates, d.npass, d.logC, used);
-        for (int q = 0; q < d.npass; ++q) {
-          const int f = d.k.pmeta[q][kS2PmFirst];
-          const int n = d.k.pmeta[q][kS2PmB] ? (d.k.pmeta[q][kS2PmCount] & 0xff) : 1;
-          fprintf(stderr, " |");
-          for (int g = f; g < f + n; ++g) {
+        for (const PPlan& pp : plan) {
+          fprintf(stderr, " |%s", pp.lanes ? "L" : "");
+          auto gate_pos = [&](int g) {
             uint32_t m = 0;
             for (int k = 0; k < d.gate[g].K; ++k) m |= (uint32_t)kdep[g][k];
             for (int k = 0; k < d.gate[g].N; ++k) m |= (uint32_t)ndep[g][k];
             fprintf(stderr, " %dx%d:", d.gate[g].K, d.gate[g].N);
             for (int b = 0; b < 16; ++b) if ((m >> b) & 1) fprintf(stderr, "%d", b);
+          };
+          if (pp.lanes) {
+            for (const auto& o : pp.ops) {
+              if (o[0] < 0) fprintf(stderr, " s%d%d", o[1] + 4, o[2]);
+              else gate_pos(o[0]);
+            }
+          } else {
+            for (int g = pp.first; g < pp.end; ++g) gate_pos(g);
           }
         }
         fprintf(stderr, "\n");
@@ -2082,19 +2223,16 @@ class Compiler {
       // (tq_sweep2.hip gate_pass_u / block_pass), so wave w owns the groups whose gi bits 6..8
       // (kS2WaveBits .. kS2LogThreads - 1, asserted in the kernel) are
       // w, i.e. the elements whose address bits behind those group bits (columns below logC, then
-      // the pass positions in ascending order) are w.  Two consecutive passes with the same
+      // the pass's group positions in its order) are w.  Two consecutive passes with the same
       // wave-select address bits leave every element with one wave: no barrier between them (LDS
-      // accesses of one wave complete in order).
+      // accesses of one wave complete in order; a lane block's swaps stay inside the wave: its
+      // lane bits are group bits 4 and 5).
       auto wave_sig = [&](int q) {
-        const uint32_t mask = (uint32_t)d.k.pmeta[q][kS2PmPass];
-        const int lg = d.logC + __builtin_popcount(mask);   // log2 groups
+        const std::vector<int>& order = plan[q].order;
+        const int lg = d.logC + (int)order.size();   // log2 groups
         std::vector<int> sig;
-        for (int b = kS2WaveBits; b < kS2LogThreads && b < lg; ++b) {
-          if (b < d.logC) { sig.push_back(-1 - b); continue; }
-          uint32_t m = mask;
-          for (int t = 0; t < b - d.logC; ++t) m &= m - 1;
-          sig.push_back(__builtin_ctz(m));
-        }
+        for (int b = kS2WaveBits; b < kS2LogThreads && b < lg; ++b)
+          sig.push_back(b < d.logC ? -1 - b : order[b - d.logC]);
         return sig;
       };
       d.nsync = 0;
@@ -2182,6 +2320,11 @@ class Compiler {
       << " chunks=" << d.nchunks << (direct ? " ->OUT" : "") << " KxN=";
     for (int j = 0; j < d.ngates; ++j) o << (j ? "," : "") << d.gate[j].K << "x" << d.gate[j].N;
     o << " passes=" << d.npass;
+    {
+      int nl = 0;
+      for (int q = 0; q < d.npass; ++q) nl += (d.k.pmeta[q][kS2PmB] & kS2PmLanes) != 0;
+      if (nl) o << " lanes=" << nl;
+    }
     if (d.epi) o << " epi";
     {
       char b[48];

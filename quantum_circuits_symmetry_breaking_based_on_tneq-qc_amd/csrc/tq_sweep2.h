@@ -75,7 +75,12 @@ struct S2Keep {
   //            A single-gate pass (B = 0) carries its gate instead: count | (K*16+N) << 8, the
   //            gate's pass mask, kaddr [4, 8), naddr [8, 16) -- a pass's head is one read batch
   //  lut rows are by PASS (row p: the group table of pass p; a block's own table)
-  int32_t pmeta[kS2MaxGates][16] = {};
+  //  A lane block (B word kS2PmLanes | 4) spans 6 positions: 4 in the registers, 2 on lane bits 4
+  //  and 5 of the thread (group-index bits 4 and 5); its codes mix gates and swap codes
+  //  (kS2SwapCode | lane bit (4: 0, 5: 1) << 2 | register bit: a register bit and a lane bit
+  //  trade positions, v_permlane16 / 32_swap), and [16, 22) hold the end layout for the
+  //  write-back: the register bits' address parts, then the XOR deltas of lane bits 4 and 5
+  int32_t pmeta[kS2MaxGates][24] = {};
 };
 
 struct S2Desc {
@@ -115,6 +120,10 @@ static_assert(kS2KeepOff % 8 == 0 && kS2DescHotBytes % 8 == 0, "descriptor copy 
 constexpr int kS2GmK = 0, kS2GmN = 1, kS2GmPass = 2, kS2GmKaddr = 3, kS2GmNaddr = kS2GmKaddr + kS2MaxK;
 static_assert(kS2GmNaddr + kS2MaxKN <= 16, "gate meta layout");
 constexpr int kS2PmFirst = 0, kS2PmCount = 1, kS2PmB = 2, kS2PmPass = 3, kS2PmAddr = 4, kS2PmCode = 8;
+constexpr int kS2PmAddrEnd = 16, kS2PmLaneDelta = 20, kS2PmWords = 24;   // lane blocks (S2Keep::pmeta)
+constexpr int kS2PmLanes = 1 << 8;     // B-word flag: a lane block
+constexpr int kS2SwapCode = 32;        // block code flag: swap a register bit with lane bit 4 / 5
+static_assert(sizeof(S2Keep::pmeta[0]) == kS2PmWords * sizeof(int32_t), "pass row words");
 constexpr int kS2PmSync = 1 << 16;   // count-word flag: a workgroup barrier before this pass
 constexpr int kS2BlkMaxGates = 8;      // gates per register block
 inline int s2_block_bits(int esz, int64_t tile_elems) {

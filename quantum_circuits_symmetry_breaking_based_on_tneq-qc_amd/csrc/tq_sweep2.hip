@@ -401,6 +401,47 @@ __device__ __forceinline__ void blk_gate(T (&x)[1 << B], const T* cf, int code) 
 #undef TQ_B2
 }
 
+// A lane block's swap (code kS2SwapCode | L << 2 | r): register bit r and lane bit 4 (L = 0) or 5
+// (L = 1) trade positions.  For every element pair (e, e | 1 << r) the pair's values transpose
+// across the two lane halves -- v_permlane16_swap (rows of 16 lanes) / v_permlane32_swap (halves
+// of the wave) on each dword: the value at (lane l, bit r = v) becomes the value that was at
+// (lane bit := v, bit r := lane bit of l)
+template <typename T, int B, int R, bool L5>
+__device__ __forceinline__ void blk_swap_rl(T (&x)[1 << B]) {
+  static_assert(sizeof(T) % 4 == 0, "dword elements");
+  constexpr int W = (int)(sizeof(T) / 4);
+#pragma unroll
+  for (int e = 0; e < (1 << B); ++e) {
+    if ((e >> R) & 1) continue;
+    union U { T t; uint32_t w[W]; } lo, hi;
+    lo.t = x[e];
+    hi.t = x[e | (1 << R)];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const auto r = L5 ? __builtin_amdgcn_permlane32_swap(lo.w[i], hi.w[i], false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo.w[i], hi.w[i], false, false);
+      lo.w[i] = r[0];
+      hi.w[i] = r[1];
+    }
+    x[e] = lo.t;
+    x[e | (1 << R)] = hi.t;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void blk_swap(T (&x)[16], int code) {
+  switch (code & 7) {
+    case 0: blk_swap_rl<T, 4, 0, false>(x); break;
+    case 1: blk_swap_rl<T, 4, 1, false>(x); break;
+    case 2: blk_swap_rl<T, 4, 2, false>(x); break;
+    case 3: blk_swap_rl<T, 4, 3, false>(x); break;
+    case 4: blk_swap_rl<T, 4, 0, true>(x); break;
+    case 5: blk_swap_rl<T, 4, 1, true>(x); break;
+    case 6: blk_swap_rl<T, 4, 2, true>(x); break;
+    default: blk_swap_rl<T, 4, 3, true>(x); break;
+  }
+}
+
 template <typename T, int B>
 __device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restrict__ cf_all, const PassHead& h,
                                            const int32_t* __restrict__ pml, const int32_t* __restrict__ lut,
@@ -423,6 +464,7 @@ __device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restr
     return o;
   };
   const int first = pm[kS2PmFirst], cnt = pm[kS2PmCount] & 0xff;
+  const bool lanes = (pm[kS2PmB] & kS2PmLanes) != 0;
   for (int g0 = threadIdx.x; g0 < ngroups; g0 += NT) {
     const int gp = g0 >> logC;
     int a0 = lut[gp & 31] ^ lut[32 + (gp >> 5)] ^ ((g0 << SH) & cmb);
@@ -431,9 +473,38 @@ __device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restr
     for (int e = 0; e < E; ++e) x[e] = *reinterpret_cast<const T*>(bb + (a0 ^ off(e)));
     // the element addresses are recomputed for the write-back (not held across the gates)
     asm volatile("" : "+v"(a0));
-    for (int q = 0; q < cnt; ++q) blk_gate<T, B>(x, cf_all + (first + q) * kCf, pml[kS2PmCode + q]);
+    // gates (and a lane block's swaps; the gate row advances on gates only)
+    int gq = first;
+    for (int q = 0; q < cnt; ++q) {
+      const int code = pml[kS2PmCode + q];
+      if constexpr (B == 4) {
+        if (code & kS2SwapCode) {
+          blk_swap<T>(x, code);
+          continue;
+        }
+      }
+      blk_gate<T, B>(x, cf_all + gq * kCf, code);
+      ++gq;
+    }
+    // write-back in the end layout (S2Keep::pmeta [16, 22): a plain block's is its start layout)
+    int be[B];
 #pragma unroll
-    for (int e = 0; e < E; ++e) *reinterpret_cast<T*>(bb + (a0 ^ off(e))) = x[e];
+    for (int b = 0; b < B; ++b) be[b] = __builtin_amdgcn_readfirstlane(pml[kS2PmAddrEnd + b]) << SH;
+    int aw = a0;
+    if (lanes) {
+      const int d4 = __builtin_amdgcn_readfirstlane(pml[kS2PmLaneDelta]) << SH;
+      const int d5 = __builtin_amdgcn_readfirstlane(pml[kS2PmLaneDelta + 1]) << SH;
+      const int lane = threadIdx.x & 63;
+      aw ^= ((lane & 16) ? d4 : 0) ^ ((lane & 32) ? d5 : 0);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      int o = 0;
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+        if ((e >> b) & 1) o ^= be[b];
+      *reinterpret_cast<T*>(bb + (aw ^ o)) = x[e];
+    }
   }
 }
 
@@ -519,7 +590,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
     if (b < oL) return true;
     if (b < oG) return (b - oL) / (64 * 4) < np;
     if (b < oP) return (b - oG) / (16 * 4) < ng;
-    return (b - oP) / (16 * 4) < np;
+    return (b - oP) / (kS2PmWords * 4) < np;
   };
   auto load_desc = [&](const S2Op& o, uint2 (&w)[kIt], Raw (&g)[kGt]) {
     const uint2* __restrict__ gd = reinterpret_cast<const uint2*>(o.desc);
@@ -777,7 +848,7 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
   // a pass's head (PassHead): the pmeta row, one batch of LDS reads into scalar registers (the
   // pass's group-table reads do not depend on it: rows by pass)
   auto read_head = [&](int p, PassHead& h) {
-    const int32_t* const pm = pmeta + p * 16;
+    const int32_t* const pm = pmeta + p * kS2PmWords;
 #pragma unroll
     for (int i = 0; i < 16; ++i) h.w[i] = __builtin_amdgcn_readfirstlane(pm[i]);
   };
@@ -851,10 +922,10 @@ __global__ void __launch_bounds__(NT, SEQ ? 1 : 4) sweep2_kernel(S2Launch L) {
       const int bk = cur.w[kS2PmB];
       const int32_t* const lp = lut + p * kLut;   // the pass's group table (rows by pass)
       if (bk == 0) run_gate<T>(buf, cf + g * kCf, cur, lp, logC);
-      else if (bk == 4) {
-        if constexpr (sizeof(T) <= 8) block_pass<T, 4>(buf, cf, cur, pmeta + p * 16, lp, logC);
+      else if ((bk & 0xff) == 4) {
+        if constexpr (sizeof(T) <= 8) block_pass<T, 4>(buf, cf, cur, pmeta + p * kS2PmWords, lp, logC);
       }
-      else block_pass<T, 3>(buf, cf, cur, pmeta + p * 16, lp, logC);
+      else block_pass<T, 3>(buf, cf, cur, pmeta + p * kS2PmWords, lp, logC);
       asm volatile("" ::: "memory");
 #ifdef TQ_S2_TIMING
       if (ch == lb && ts_rec && threadIdx.x == 0 && p < 16) {
