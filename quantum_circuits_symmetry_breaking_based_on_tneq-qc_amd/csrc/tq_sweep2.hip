@@ -489,9 +489,11 @@ __device__ __forceinline__ void block_pass(T* __restrict__ buf, const T* __restr
     // write-back in the end layout (S2Keep::pmeta [16, 22): a plain block's is its start layout)
     int be[B];
 #pragma unroll
-    for (int b = 0; b < B; ++b) be[b] = __builtin_amdgcn_readfirstlane(pml[kS2PmAddrEnd + b]) << SH;
+    for (int b = 0; b < B; ++b) be[b] = ba[b];
     int aw = a0;
     if (lanes) {
+#pragma unroll
+      for (int b = 0; b < B; ++b) be[b] = __builtin_amdgcn_readfirstlane(pml[kS2PmAddrEnd + b]) << SH;
       const int d4 = __builtin_amdgcn_readfirstlane(pml[kS2PmLaneDelta]) << SH;
       const int d5 = __builtin_amdgcn_readfirstlane(pml[kS2PmLaneDelta + 1]) << SH;
       const int lane = threadIdx.x & 63;
