@@ -49,3 +49,36 @@ def test_relisting_never_adds_passes():
             assert p1 <= p0, (cfg, p1, p0)
     # C2's chains leave room: strictly fewer passes overall (r06: 216 -> 209)
     assert sum(p for _, p, _ in on["C2"] if p > 0) < sum(p for _, p, _ in off["C2"] if p > 0)
+
+
+_LANES = r"""
+import json, sys, torch
+sys.path.insert(0, sys.argv[1])
+from tneq_qc_amd.circuits import config_task, with_batch
+from tneq_qc_amd.expression import HipContractExpression
+t = with_batch(config_task("C4"), 0)
+e = HipContractExpression(t.eq, *t.shapes, optimize=t.path, slices=t.sliced)
+d = e.plan(torch.complex64).describe().splitlines()
+s2 = [l for l in d if " SWEEP2 " in l and "passes=" in l]
+print(json.dumps({"passes": sum(int(l.split("passes=")[1].split()[0]) for l in s2),
+                  "lanes": sum(int(l.split("lanes=")[1].split()[0]) for l in s2 if "lanes=" in l),
+                  "ops": len(s2)}))
+"""
+
+
+@pytest.mark.timeout(600)
+def test_lane_blocks_are_opt_in_and_cut_passes():
+    """TQ_S2_LANEBLK=1 (lane blocks: 6-position register blocks over 4 lanes, tq_plan.cpp
+    lane_span) compiles C4 with lane passes and fewer passes than the default, which has none
+    (r06: C4's big sweep ops 174 -> 125 passes).  Parity of the opt-in path: test_laneblk_gpu.py."""
+    import json
+    res = {}
+    for on in (0, 1):
+        env = dict(os.environ, TQ_S2_LANEBLK=str(on))
+        r = subprocess.run([sys.executable, "-c", _LANES, ROOT], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[on] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res[0]["lanes"] == 0 and res[1]["lanes"] > 0
+    assert res[1]["ops"] == res[0]["ops"]
+    assert res[1]["passes"] < res[0]["passes"]
