@@ -273,6 +273,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--one-stream", action="store_true", help="candidates one after another on one stream")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="candidate k on stream k mod N (0: one stream per candidate)")
     ap.add_argument("--eager", action="store_true",
                     help="forward / loss / backward issued eagerly every step (default: one hipGraph per candidate)")
     ap.add_argument("--port", type=int, default=0, help="gloo timing group port (multi-rank)")
@@ -292,7 +294,11 @@ def main():
     mine = list(range(rank, len(CANDIDATES), world))
     _log(f"rank {rank}: setting up {len(mine)} candidates")
     target, cands = setup(dev, set(mine))
-    streams = None if a.one_stream else [torch.cuda.Stream(dev) for _ in cands]
+    if a.one_stream:
+        streams = None
+    else:
+        pool = [torch.cuda.Stream(dev) for _ in range(a.streams if a.streams > 0 else len(cands))]
+        streams = [pool[k % len(pool)] for k in range(len(cands))]
     graph_all = capture_all(target, cands, dev) if a.one_graph else None
     graphs = None if (a.eager or a.one_graph) else capture(target, cands, dev)
     step = (lambda: gpu_step_one_graph(target, cands, graph_all)) if graph_all else \
@@ -330,7 +336,7 @@ def main():
            "n_gpus": world, "candidates": len(CANDIDATES),
            "candidates_per_rank": [len(range(r, len(CANDIDATES), world)) for r in range(world)],
            "cores_per_candidate": len(cands[0][1]), "dtype": "c128",
-           "streams": len(streams) if streams else 1,
+           "streams": len({id(x) for x in streams}) if streams else 1,
            "step_graphs": "one graph, a branch per candidate" if graph_all else graphs is not None,
            "forward": "QCTN.split halves swept + boundary contraction (split/merge path), one native plan",
            "amplitudes_per_forward": int(np.prod(cands[0][0].out_shape)),
